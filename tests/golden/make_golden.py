@@ -1,0 +1,222 @@
+"""Generate the golden parity fixtures from the REAL reference arithmetic.
+
+Run in the build container (NOT on the GPU box; it needs /root/reference and the
+HF Transformers oracle):   python tests/golden/make_golden.py
+
+What produces each vector:
+  * HF Transformers 5.15 `WhisperFeatureExtractor` (the reference's log-mel,
+    `training/run_distillation.py:1217`)                                -> mel.npz
+  * HF `WhisperForConditionalGeneration` fp32 on the micro config with the
+    documented PRNG weights (oracle/weights.py); the reference's train_step
+    arithmetic (`run_distillation.py:1507-1551`) applied to the HF outputs, the
+    HF-model autograd backward and torch clip_grad_norm_ + AdamW
+    (`:1425-1455,1666-1668`)                                            -> micro_step.npz
+  * the reference's own `init_student_model_from_teacher`
+    (`training/create_student_model.py:99-226`, imported from /root/reference)
+    and `mix_language_embeddings` (`utils/model_utils.py:4-14`)         -> student.npz
+  * HF `generate(num_beams=1)` greedy with forced prompt                 -> greedy.npz
+
+Only small slices / checksums are stored (fixtures are data, no reference source).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle import labels as L  # noqa: E402
+from oracle import logmel  # noqa: E402
+from oracle.weights import CONFIGS, SPECIAL, make_weights  # noqa: E402
+
+REF = "/root/reference"
+# large-v2 generation_config.suppress_tokens (test parameter for the suppress processor)
+SUPPRESS = [1, 2, 7, 8, 9, 10, 14, 25, 26, 27, 28, 29, 31, 58, 59, 60, 61, 62, 63, 90, 91, 92, 93,
+            359, 503, 522, 542, 873, 893, 902, 918, 922, 931, 1350, 1853, 1982, 2460, 2627, 3246,
+            3253, 3268, 3536, 3846, 3961, 4183, 4667, 6585, 6647, 7273, 9061, 9383, 10428, 10929,
+            11938, 12033, 12331, 12562, 13793, 14157, 14635, 15265, 15618, 16553, 16604, 18362,
+            18956, 20075, 21675, 22520, 26130, 26161, 26435, 28279, 29464, 31650, 32302, 32470,
+            36865, 42863, 47425, 49870, 50254, 50258, 50358, 50359, 50360, 50361, 50362]
+ROWS = [0, 3, 4, 57, 200, 446]          # decoder positions whose full logit rows are checked
+VSTRIDE = 97                             # vocab subsample stride for stored logit rows
+
+
+def hf_model(cfg, w, dtype=torch.float32):
+    from transformers import WhisperConfig, WhisperForConditionalGeneration
+    m = WhisperForConditionalGeneration(WhisperConfig(**cfg))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()}, strict=False)
+    assert m.proj_out.weight.data_ptr() == m.model.decoder.embed_tokens.weight.data_ptr()
+    return m.to(dtype)
+
+
+def micro_batch():
+    feats = logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(1, 17.0)])
+    lists = L.synthetic_label_lists(2, seed=0)
+    # force a <|startofprev|> prompt on clip 1 (exercise the A7 teacher-input quirk)
+    lists[1] = [SPECIAL["startofprev"], 11, 12, 13] + lists[1][:200]
+    dec, lab = L.collate(lists)
+    return feats, dec, lab, lists
+
+
+def gen_mel(out):
+    from transformers import WhisperFeatureExtractor
+    fe = WhisperFeatureExtractor()
+    clips = [logmel.synthetic_clip(0), logmel.synthetic_clip(3, 12.0), logmel.synthetic_clip(5, 45.0)]
+    clips.append(np.zeros(16000, dtype=np.float32))   # silent clip: floor path
+    mel = fe(clips, sampling_rate=16000, return_tensors="np").input_features.astype(np.float32)
+    out["mel_sub"] = mel[:, :, ::10]
+    out["mel_rowsum"] = mel.sum(-1)
+    out["mel_max"] = mel.reshape(len(clips), -1).max(-1)
+    out["mel_filters"] = fe.mel_filters.astype(np.float32)
+
+
+def gen_micro(out):
+    from transformers.modeling_outputs import BaseModelOutput
+    cfg = CONFIGS["micro"]
+    ws, wt = make_weights(cfg, 1), make_weights(cfg, 2)
+    S, Tm = hf_model(cfg, ws), hf_model(cfg, wt)
+    feats, dec, lab, _ = micro_batch()
+    feats_t, dec_t, lab_t = torch.from_numpy(feats), torch.from_numpy(dec), torch.from_numpy(lab)
+    out["feats"], out["dec"], out["lab"] = feats, dec, lab
+    S.eval(); Tm.eval()
+    # freeze student encoder (c3 recipe: share_hidden_states, run_distillation.py:1043-1075)
+    for p in S.model.encoder.parameters():
+        p.requires_grad_(False)
+    S.model.decoder.embed_positions.weight.requires_grad_(False)
+    so = S(input_features=feats_t, decoder_input_ids=dec_t, labels=lab_t)
+    with torch.no_grad():
+        to_share = Tm(encoder_outputs=BaseModelOutput(so.encoder_last_hidden_state.detach()), labels=lab_t)
+        to_full = Tm(input_features=feats_t, decoder_input_ids=dec_t, labels=lab_t)
+    T = 2.0
+
+    def kl_of(t_logits):
+        p = torch.softmax(t_logits / T, -1)
+        lq = torch.log_softmax(so.logits / T, -1)
+        div = torch.nn.functional.kl_div(lq, p, reduction="none") * (lab_t >= 0).unsqueeze(-1)
+        return div.sum() / (lab_t >= 0).sum() * T ** 2
+
+    kl_share, kl_full = kl_of(to_share.logits), kl_of(to_full.logits)
+    loss = 0.8 * so.loss + 1.0 * kl_share
+    out["ce"], out["kl_share"], out["kl_full"], out["loss"] = [np.float64(x.item()) for x in
+                                                               (so.loss, kl_share, kl_full, loss)]
+    out["enc_sub"] = so.encoder_last_hidden_state.detach().numpy()[:, ::50, :]
+    lg = so.logits.detach()
+    out["s_lse"] = torch.logsumexp(lg, -1).numpy()
+    out["s_argmax"] = lg.argmax(-1).numpy()
+    out["s_rows"] = lg[:, ROWS, ::VSTRIDE].numpy()
+    out["t_share_lse"] = torch.logsumexp(to_share.logits, -1).numpy()
+    out["t_share_rows"] = to_share.logits[:, ROWS, ::VSTRIDE].numpy()
+    out["t_full_lse"] = torch.logsumexp(to_full.logits, -1).numpy()
+    loss.backward()
+    names = [n for n, p in S.named_parameters() if p.requires_grad]
+    out["grad_names"] = np.array(names)
+    out["grad_norms"] = np.array([S.get_parameter(n).grad.norm().item() for n in names])
+    g = S.model.decoder.layers[1].fc2.weight.grad
+    out["grad_dec1_fc2_sub"] = g[::7, ::11].clone().numpy()
+    out["grad_embed_rows"] = S.model.decoder.embed_tokens.weight.grad[[50258, 50260, 50363, 11, 12]].clone().numpy()
+    # clip + AdamW (lr 1e-4) one update, as the reference loop does on the sync step
+    tp = [S.get_parameter(n) for n in names]
+    gn = torch.nn.utils.clip_grad_norm_(tp, 1.0)
+    opt = torch.optim.AdamW(tp, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
+    opt.step()
+    out["grad_total_norm"] = np.float64(gn.item())
+    out["upd_dec0_q_sub"] = S.model.decoder.layers[0].self_attn.q_proj.weight.detach()[::5, ::5].numpy()
+    out["upd_embed_row"] = S.model.decoder.embed_tokens.weight.detach()[[50260, 100]].numpy()
+
+
+def gen_student(out):
+    sys.path.insert(0, REF)
+    sys.path.insert(0, os.path.join(REF, "training"))
+    import create_student_model as csm      # reference module (imports utils.model_utils)
+    from transformers import WhisperFeatureExtractor
+
+    class _Proc:  # tokenizer files are absent offline: stub processor
+        def __init__(self):
+            self.feature_extractor = WhisperFeatureExtractor()
+            self.tokenizer = types.SimpleNamespace(
+                convert_tokens_to_ids=lambda t: {"<|en|>": SPECIAL["en"], "<|zh|>": SPECIAL["zh"]}[t])
+
+        @classmethod
+        def from_pretrained(cls, *a, **k):
+            return cls()
+
+        def save_pretrained(self, *a, **k):
+            pass
+
+        def __call__(self, audio, sampling_rate=16000, return_tensors="pt"):
+            return self.feature_extractor(audio, sampling_rate=sampling_rate, return_tensors=return_tensors)
+
+    csm.WhisperProcessor = _Proc
+    from transformers import GenerationConfig
+    cfg = dict(CONFIGS["micro"], encoder_layers=4, decoder_layers=5)
+    w = make_weights(cfg, 7)
+    tmp = tempfile.mkdtemp()
+    tdir, sdir = os.path.join(tmp, "teacher"), os.path.join(tmp, "student")
+    hf_model(cfg, w).save_pretrained(tdir)
+    GenerationConfig(decoder_start_token_id=SPECIAL["sot"]).save_pretrained(tdir)
+    cases = {"e2_d2": dict(encoder_layers=2, decoder_layers=2),
+             "d3": dict(decoder_layers=3),
+             "e3_dnums": dict(encoder_layers=3, decoder_layers=2, decoder_layers_numbers=[1, 4]),
+             "mix": dict(encoder_layers=2, decoder_layers=2, mix_lang_emb=True)}
+    from safetensors.numpy import load_file
+    meta = {}
+    for name, kw in cases.items():
+        d = sdir + "_" + name
+        csm.init_student_model_from_teacher(tdir, save_dir=d, **kw)
+        sd = load_file(os.path.join(d, "model.safetensors"))
+        scfg = json.load(open(os.path.join(d, "config.json")))
+        meta[name] = dict(encoder_layers=scfg["encoder_layers"], decoder_layers=scfg["decoder_layers"],
+                          keys=sorted(sd))
+        for k in sorted(sd):
+            out[f"{name}|{k}"] = np.float64(np.asarray(sd[k], dtype=np.float64).sum())
+    out["student_meta"] = np.array(json.dumps(meta))
+    # mix_language_embeddings on a bf16 teacher (the reference's teacher dtype, :1019-1020)
+    from utils.model_utils import mix_language_embeddings
+    m = hf_model(cfg, w).to(torch.bfloat16)
+    tok = types.SimpleNamespace(convert_tokens_to_ids=lambda t: {"<|en|>": SPECIAL["en"], "<|zh|>": SPECIAL["zh"]}[t])
+    mix_language_embeddings(m, tok, languages=["zh", "en"])
+    out["mix_bf16_row_u16"] = m.model.decoder.embed_tokens.weight[SPECIAL["zh"]].view(torch.int16).numpy()
+    m32 = hf_model(cfg, w)
+    mix_language_embeddings(m32, tok, languages=["en", "zh"], weights=[0.5, 0.5])
+    out["mix_f32_row"] = m32.model.decoder.embed_tokens.weight[SPECIAL["zh"]].detach().numpy()
+
+
+def gen_greedy(out):
+    from transformers import GenerationConfig
+    cfg = CONFIGS["micro"]
+    m = hf_model(cfg, make_weights(cfg, 1, lin_std=0.2)).eval()   # stronger layers: non-trivial decode
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0),
+                                                   logmel.synthetic_clip(4, 25.0)]))
+    prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
+    gc = GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
+                          pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
+                          begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=64, num_beams=1,
+                          do_sample=False, no_timestamps_token_id=SPECIAL["notimestamps"])
+    m.generation_config = gc
+    with torch.no_grad():
+        ids = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * 3), max_length=64,
+                         num_beams=1, do_sample=False)
+    out["greedy_ids"] = ids.numpy()        # HF returns the generated tokens only (prompt stripped)
+    out["greedy_prompt"] = np.array(prompt)
+    out["suppress"] = np.array(SUPPRESS)
+
+
+def main():
+    torch.manual_seed(0)
+    for name, fn in (("mel", gen_mel), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy)):
+        out = {}
+        fn(out)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+        print(name, {k: getattr(v, "shape", None) for k, v in list(out.items())[:12]})
+
+
+if __name__ == "__main__":
+    main()

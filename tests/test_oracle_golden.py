@@ -1,0 +1,155 @@
+"""Pin the oracle against the golden vectors made from the real reference arithmetic
+(tests/golden/make_golden.py).  CPU only."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import distill_ref, greedy_ref, labels as L, logmel, student_ref
+from oracle.weights import CONFIGS, SPECIAL, make_weights
+from oracle.whisper_ref import Ref, to_torch
+
+
+def test_mel_filterbank_exact():
+    g = load_golden("mel")
+    np.testing.assert_allclose(logmel.mel_filter_bank().astype(np.float32), g["mel_filters"], rtol=0, atol=1e-7)
+
+
+def test_logmel_matches_hf():
+    g = load_golden("mel")
+    clips = [logmel.synthetic_clip(0), logmel.synthetic_clip(3, 12.0), logmel.synthetic_clip(5, 45.0),
+             np.zeros(16000, dtype=np.float32)]
+    mel = logmel.log_mel_batch(clips)
+    # HF runs torch.stft in fp32; the oracle is float64 -> 2e-4 abs (values O(1))
+    np.testing.assert_allclose(mel[:, :, ::10], g["mel_sub"], atol=2e-4, rtol=0)
+    np.testing.assert_allclose(mel.max(axis=(1, 2)), g["mel_max"], atol=2e-4)
+
+
+def test_collator_prompt_quirk():
+    """SURVEY.md finding 3: student vs teacher decoder inputs with a prompt."""
+    sot, zh, tr, nt = SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]
+    seq = [50361, 11, 12, 13, sot, zh, tr, nt, 100, 200, 300, SPECIAL["eot"]]
+    dec, lab = L.collate([seq], max_target_length=12)
+    assert dec[0].tolist() == seq[:-1]
+    assert lab[0].tolist()[:4] == [-100] * 4 and lab[0, 4] == zh
+    tin = L.shift_tokens_right(lab)
+    assert tin[0].tolist()[:10] == [50258, 50257, 50257, 50257, 50257, 50260, 50359, 50363, 100, 200]
+    # no prompt: teacher input == student input
+    seq2 = [sot, zh, tr, nt, 5, 6, SPECIAL["eot"]]
+    dec2, lab2 = L.collate([seq2], max_target_length=10)
+    assert L.shift_tokens_right(lab2)[0].tolist() == dec2[0].tolist()
+    assert lab2[0].tolist() == [zh, tr, nt, 5, 6, 50257, -100, -100, -100]
+
+
+def test_prepare_labels_timestamp_and_prompt_paths():
+    rng = np.random.RandomState(0)
+    ts = SPECIAL["timestamp_begin"]
+    toks = [[SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], ts, 5, 6, ts + 50, SPECIAL["eot"]]] * 6
+    prev = [[7, 8, ts + 3, 9]] * 6
+    out = L.prepare_labels(toks, prev, rng, timestamp_probability=0.5, condition_on_prev_probability=0.5)
+    r2 = np.random.RandomState(0)
+    for o in out:
+        pred_ts = bool(r2.binomial(1, 0.5)); cond = bool(r2.binomial(1, 0.5))
+        body = toks[0] if pred_ts else [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"], 5, 6,
+                                          SPECIAL["eot"]]
+        if cond:
+            p = prev[0] if pred_ts else [7, 8, 220, 9]
+            body = p + body
+        assert o == body
+
+
+@pytest.fixture(scope="module")
+def micro():
+    g = load_golden("micro_step")
+    cfg = CONFIGS["micro"]
+    return g, cfg, make_weights(cfg, 1), make_weights(cfg, 2)
+
+
+def test_micro_forward_matches_hf(micro):
+    g, cfg, ws, wt = micro
+    S, T = Ref(cfg, to_torch(ws)), Ref(cfg, to_torch(wt))
+    feats, dec, lab = (torch.from_numpy(g[k]) for k in ("feats", "dec", "lab"))
+    with torch.no_grad():
+        s = S.forward(feats, dec, lab)
+        t_share = T.forward(enc=s["enc"], labels=lab)
+        t_full = T.forward(feats, dec, lab)
+    np.testing.assert_allclose(s["enc"].numpy()[:, ::50], g["enc_sub"], atol=2e-5)
+    np.testing.assert_allclose(torch.logsumexp(s["logits"], -1).numpy(), g["s_lse"], rtol=1e-5)
+    np.testing.assert_allclose(s["logits"][:, [0, 3, 4, 57, 200, 446], ::97].numpy(), g["s_rows"], atol=5e-5)
+    np.testing.assert_array_equal(s["logits"].argmax(-1).numpy(), g["s_argmax"])
+    np.testing.assert_allclose(torch.logsumexp(t_share["logits"], -1).numpy(), g["t_share_lse"], rtol=1e-5)
+    np.testing.assert_allclose(torch.logsumexp(t_full["logits"], -1).numpy(), g["t_full_lse"], rtol=1e-5)
+    # the A7 quirk: teacher(encoder_outputs, labels) == teacher(dec ids) except on the prompted clip
+    with torch.no_grad():
+        t_dec = T.forward(enc=s["enc"], decoder_input_ids=dec)
+    a, b = torch.logsumexp(t_dec["logits"], -1).numpy(), g["t_share_lse"]
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-5)
+    assert not np.allclose(a[1], b[1], rtol=1e-4)
+    ce = float(s["loss"])
+    assert abs(ce - float(g["ce"])) / float(g["ce"]) < 1e-5
+    _, kl = distill_ref.distill_loss(s["logits"], t_share["logits"], lab, s["loss"])
+    assert abs(float(kl) - float(g["kl_share"])) / float(g["kl_share"]) < 1e-4
+
+
+def test_micro_train_step_grads_and_adamw(micro):
+    g, cfg, ws, wt = micro
+    ps = to_torch(ws)
+    names = [str(n) for n in g["grad_names"]]
+    for n in names:
+        ps[n].requires_grad_(True)
+    S, T = Ref(cfg, ps), Ref(cfg, to_torch(wt))
+    feats, dec, lab = (torch.from_numpy(g[k]) for k in ("feats", "dec", "lab"))
+    out = distill_ref.train_step(S, T, feats, dec, lab)
+    assert abs(float(out["loss"]) - float(g["loss"])) / float(g["loss"]) < 1e-5
+    norms = np.array([ps[n].grad.norm().item() for n in names])
+    np.testing.assert_allclose(norms, g["grad_norms"], rtol=2e-4, atol=1e-9)
+    np.testing.assert_allclose(ps["model.decoder.layers.1.fc2.weight"].grad[::7, ::11].numpy(),
+                               g["grad_dec1_fc2_sub"], rtol=1e-3, atol=1e-8)
+    gn, _ = distill_ref.optimizer_step(ps, names, lr=1e-4, frozen_prefixes=("model.encoder",))
+    assert abs(float(gn) - float(g["grad_total_norm"])) / float(g["grad_total_norm"]) < 1e-4
+    np.testing.assert_allclose(ps["model.decoder.layers.0.self_attn.q_proj.weight"].detach()[::5, ::5].numpy(),
+                               g["upd_dec0_q_sub"], atol=1e-6)
+    np.testing.assert_allclose(ps["model.decoder.embed_tokens.weight"].detach()[[50260, 100]].numpy(),
+                               g["upd_embed_row"], atol=1e-6)
+
+
+def test_student_init_matches_reference():
+    g = load_golden("student")
+    meta = json.loads(str(g["student_meta"]))
+    cfg = dict(CONFIGS["micro"], encoder_layers=4, decoder_layers=5)
+    w = make_weights(cfg, 7)
+    cases = {"e2_d2": dict(encoder_layers=2, decoder_layers=2), "d3": dict(decoder_layers=3),
+             "e3_dnums": dict(encoder_layers=3, decoder_layers=2, decoder_layers_numbers=[1, 4])}
+    for name, kw in cases.items():
+        scfg, sd, _, _ = student_ref.init_student_from_teacher(cfg, w, **kw)
+        assert scfg["encoder_layers"] == meta[name]["encoder_layers"]
+        assert scfg["decoder_layers"] == meta[name]["decoder_layers"]
+        assert sorted(sd) == meta[name]["keys"]
+        for k in sd:
+            assert abs(float(np.asarray(sd[k], np.float64).sum()) - float(g[f"{name}|{k}"])) < 1e-6, (name, k)
+    # mix_lang_emb (student creation mixes en,zh @0.5 in fp32)
+    scfg, sd, _, _ = student_ref.init_student_from_teacher(cfg, w, encoder_layers=2, decoder_layers=2)
+    emb = sd["model.decoder.embed_tokens.weight"]
+    student_ref.mix_language_embeddings(emb, [SPECIAL["en"], SPECIAL["zh"]], SPECIAL["zh"], [0.5, 0.5])
+    for k in sd:
+        assert abs(float(np.asarray(sd[k], np.float64).sum()) - float(g[f"mix|{k}"])) < 1e-6, k
+    np.testing.assert_array_equal(emb[SPECIAL["zh"]], g["mix_f32_row"])
+
+
+def test_greedy_matches_hf_generate():
+    g = load_golden("greedy")
+    cfg = CONFIGS["micro"]
+    m = Ref(cfg, to_torch(make_weights(cfg, 1, lin_std=0.2)))
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0),
+                                                   logmel.synthetic_clip(4, 25.0)]))
+    with torch.no_grad():
+        ids = greedy_ref.greedy(m, feats, g["greedy_prompt"].tolist(), max_length=64,
+                                suppress_tokens=g["suppress"].tolist())
+    ref = g["greedy_ids"]                       # generated tokens only
+    gen = ids.numpy()[:, len(g["greedy_prompt"]):]
+    n = min(gen.shape[1], ref.shape[1])
+    assert n >= 32
+    np.testing.assert_array_equal(gen[:, :n], ref[:, :n])
+    assert len(set(ref[:, :4].ravel().tolist())) > 3    # fixture is not a degenerate repeat
