@@ -1,0 +1,111 @@
+/*
+ * tw_hip.h — C-ABI of libtw_hip.so, the MI355X (gfx950) kernels behind the taiwan-whisper
+ * distillation hot path.
+ *
+ * The reference has no native plugin API: its hot path calls HF
+ * Transformers / ATen / cuBLAS / SDPA / NCCL implicitly.  Each entry point below replaces
+ * one of those implicit kernels and cites the reference line that triggers it.  The
+ * Python host package (taiwan-whisper_amd/tw) binds these with ctypes; INTEGRATION.md shows
+ * the binding a maintainer would add on the reference side.
+ *
+ * Conventions
+ *   - plain device pointers, int64 leading dimensions in ELEMENTS, row-major;
+ *   - dtype codes: 0 = fp32, 1 = bf16;
+ *   - every call is stream-ordered on `stream` (a hipStream_t), never synchronises,
+ *     never allocates; workspaces are caller-provided;
+ *   - return 0 on success, 1 = invalid argument/shape, 2 = unsupported, 3 = HIP launch error;
+ *   - the library holds no global mutable state; calls are reentrant.
+ */
+#ifndef TW_HIP_H
+#define TW_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* tw_stream_t; /* hipStream_t */
+
+/* GEMM flags */
+#define TW_GEMM_BIAS 1
+#define TW_GEMM_ROUND 2
+#define TW_GEMM_GELU 4
+#define TW_GEMM_RES 8
+#define TW_GEMM_ACCUM 16
+#define TW_GEMM_AUX_OUT 32
+#define TW_GEMM_DGELU 64
+
+/* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
+ * Replaces every nn.Linear / Conv1d (as GEMM) / tied proj_out matmul of the step, forward and
+ * backward: HF modeling_whisper.py:279-345 (q/k/v/out_proj), :618-619 (conv1/conv2), :400-410 and
+ * :495-505 (fc1 + GELU + fc2), :1080 (proj_out); run_distillation.py:1528,1534,1665 (fwd, teacher fwd, backward).
+ * Epilogue order: +bias[n] (bf16) -> ROUND to bf16 -> DGELU (x gelu'(aux)) -> GELU (aux <- pre-act)
+ *   -> +res[m % res_mod][n] -> +C_old (ACCUM) -> store as c_dtype.  K % 8 == 0 unless both operands are MN-major; a_trans needs M % 8 == 0,
+ *   b_trans needs N % 8 == 0; lda, ldb % 8 == 0; A, B 16-byte aligned. */
+int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans, void* C,
+                 int64_t ldc, int c_dtype, int M, int N, int K, int batch, int64_t sA, int64_t sB, int64_t sC,
+                 float alpha, const void* bias, const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
+                 void* aux, int64_t ldaux, int64_t sAux, int flags, tw_stream_t stream);
+
+/* LayerNorm fp32-statistics forward / backward (D % 64 == 0, D <= 1280).
+ * Replaces nn.LayerNorm at HF modeling_whisper.py:392,402,470,485,498,642,790 (autocast fp32 op). */
+int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, const float* b, void* y, int y_dtype,
+                     float* mean_out, float* rstd_out, int rows, int D, float eps, tw_stream_t stream);
+int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd, const void* dy,
+                     int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out, int rows, int D,
+                     float* workspace, int64_t workspace_floats, tw_stream_t stream);
+
+/* Flash attention, head_dim 64, bf16 (replaces SDPA at HF modeling_whisper.py:337-350 for encoder
+ * self-attn, decoder causal self-attn and cross-attn).  lse: [B][H][Tq] fp32 (natural log). */
+int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv, void* O,
+                int64_t ldo, float* lse, int B, int H, int Tq, int Tk, int head_dim, int causal, float scale,
+                tw_stream_t stream);
+int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv, const void* O,
+                int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ, int64_t lddq, void* dK,
+                int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq, int Tk, int head_dim, int causal,
+                float scale, float* workspace /* B*H*Tq floats */, tw_stream_t stream);
+
+/* Fused CE + temperature KL loss and its logits gradient (replaces run_distillation.py:1507-1516,
+ * :1539-1549 and HF CE :1082-1087).  out3 = [loss, ce, kl*T^2]; dlogits may be NULL. */
+int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, const int64_t* labels, int64_t rows, int V,
+             float T, float ce_w, float kl_w, const int* n_valid, float grad_scale, float* row_out, float* out3,
+             void* dlogits, tw_stream_t stream);
+
+/* Whisper log-mel (replaces WhisperFeatureExtractor at run_distillation.py:1217).
+ * wav [B][480000] fp32 -> mel_out [B][80][3000] fp32 and optional conv1 input [B][3002][80] bf16. */
+int tw_logmel(const float* wav, int B, const float* basis, const int* mel_start, const float* mel_w, float* mel_out,
+              void* conv_in, void* workspace /* B uint32 */, tw_stream_t stream);
+int tw_mel_to_conv_input(const float* mel, void* xt, int B, int nmel, int T, tw_stream_t stream);
+
+/* Decoder token + learned position embedding (HF modeling_whisper.py:736,754-761) and its
+ * scatter-add backward into the tied embedding gradient. */
+int tw_embed_fwd(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
+                 int out_dtype, int rows, int T, int pos_offset, int D, tw_stream_t stream);
+int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D, tw_stream_t stream);
+
+/* autocast weight cast fp32 -> bf16 (ACC:accelerator.py autocast of every Linear weight). */
+int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, tw_stream_t stream);
+/* bias gradient: out[c] (+)= [bf16](sum_r x[r][c]). */
+int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum, int round_bf16,
+              tw_stream_t stream);
+
+/* clip_grad_norm_ + AdamW (run_distillation.py:1450-1455,1666-1668). */
+int tw_l2norm(const float* x, int64_t n, float* norm_out, float* workspace /* 1024 floats */, tw_stream_t stream);
+int tw_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float b1, float b2,
+             float eps, float wd, int step, const float* norm, float max_norm, tw_stream_t stream);
+int tw_clip_scale(float* x, int64_t n, const float* norm, float max_norm, tw_stream_t stream);
+
+/* conv-stem backward helpers (HF modeling_whisper.py:618-619). */
+int tw_im2col3(const void* src, int64_t src_rows, void* dst, int B, int T_out, int stride, int C,
+               tw_stream_t stream);
+int tw_col2im_s2(const float* dA, float* dX, int B, int T_in, int T_out, int C, tw_stream_t stream);
+
+/* teacher decoder input = shift_tokens_right(labels) (run_distillation.py:1534, HF modeling_whisper.py:68-81);
+ * number of labels >= 0 (kl_divergence normaliser, run_distillation.py:1512-1515). */
+int tw_shift_tokens_right(const int64_t* labels, int64_t* out, int B, int T, int64_t pad, int64_t start,
+                          tw_stream_t stream);
+int tw_count_valid(const int64_t* labels, int64_t n, int* out, tw_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TW_HIP_H */

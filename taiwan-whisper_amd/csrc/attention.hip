@@ -1,0 +1,521 @@
+// Flash attention, head dim 64, bf16 in/out, fp32 softmax:
+//   encoder self-attention (1500 x 1500), decoder causal self-attention (447 x 447) and
+//   cross-attention (447 x 1500) of HF WhisperAttention (modeling_whisper.py:265-350;
+//   q pre-scaled by hd^-0.5 -> here `scale` is applied to the fp32 scores, identical
+//   because 2^-3 scaling is exact).
+//
+// Layout: rows of [B*T][ld] with head h at columns h*64 .. h*64+63, so Q/K/V are read
+// in place from the fused QKV (or KV) projection output and O is written where out_proj
+// reads it.  LSE [B][H][Tq] (natural log of the scaled-score row sum) is kept for the
+// backward pass.
+//
+// MFMA v_mfma_f32_16x16x32_bf16 in the "swapped" orientation: S^T = K·Q^T, so each lane
+// holds 4 keys of one query; the probabilities then ARE the B operand of O^T = V^T·P^T
+// (accumulator-as-operand, keys in permuted order 4g+r / 16+4g+r) and V^T comes from
+// ds_read_b64_tr_b16 reads of a row-major V tile.  Every LDS tile is [64 rows][64] bf16
+// with 16-B chunk c of row r stored at c ^ (r & 7): conflict-free for both the ds_read_b128
+// row reads and the transposed reads.
+#include "common.h"
+
+namespace {
+
+constexpr int QW = 32;          // query rows per wave
+constexpr int QB = 4 * QW;      // query rows per workgroup
+constexpr int KT = 64;          // keys per LDS tile
+constexpr int TB = KT * 64 * 2; // bytes per [64][64] bf16 tile
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+// [64 rows][64 cols] tile from rows row0.. of a [rows][ld] matrix; rows >= rows_valid read 0.
+__device__ __forceinline__ void stage_tile(const bf16* base, int64_t ld, int rows_valid, char* lds, int wave,
+                                           int lane) {
+  const auto rs = make_rsrc(base);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pce = wave + 4 * i;
+    const int r = pce * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const uint32_t off = r < rows_valid ? (uint32_t)(((int64_t)r * ld + c * 8) * 2) : TW_OOB;
+    buf_load_lds16(rs, lds + pce * 1024, off);
+  }
+}
+
+// row fragment: lane gives T[rbase + (l&15)][kk*32 + 8*(l>>4) .. +7]
+__device__ __forceinline__ bf16x8 rd_row(const char* t, int rbase, int kk, int lane) {
+  const int r = rbase + (lane & 15);
+  return *(const bf16x8*)(t + swz(r, kk * 4 + (lane >> 4)));
+}
+
+// transposed fragment for k-step s over rows: lane gives T^T[cbase + i][rows perm(s)]
+//   elements 0..3: rows s*32 + 4g + 0..3 ; elements 4..7: rows s*32 + 16 + 4g + 0..3
+__device__ __forceinline__ bf16x8 rd_tr(const char* t, int cbase, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int col = cbase + 4 * (i & 3);
+  const int r0 = s * 32 + 4 * g + (i >> 2);
+  const int r1 = r0 + 16;
+  const int ch = col >> 3, inoff = (col & 7) * 2;
+  const char* a0 = t + swz(r0, ch) + inoff;
+  const char* a1 = t + swz(r1, ch) + inoff;
+  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a1);
+  s16x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// global fragment: lane gives M[row0 + (l&15)][kk*32 + 8*(l>>4) .. +7] (zero past rows_valid)
+__device__ __forceinline__ bf16x8 ld_frag(const bf16* base, int64_t ld, int row, int rows_valid, int kk, int lane) {
+  if (row >= rows_valid) return bf16x8{};
+  return *(const bf16x8*)(base + (int64_t)row * ld + kk * 32 + 8 * (lane >> 4));
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  return bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+struct AttnP {
+  const bf16* Q; const bf16* K; const bf16* V; bf16* O; float* lse;
+  const bf16* dO; const float* Dv; bf16* dQ; bf16* dK; bf16* dV;
+  int64_t ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
+  int B, H, Tq, Tk, causal;
+  float scale, scale_log2;
+};
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1e30f;
+
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // [2 stages][K, V]
+  const int lane = lane_id(), wave = wave_id_uniform();
+  const int g = lane >> 4, li = lane & 15;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int qblk = blockIdx.x * QB;
+  const int qw = qblk + wave * QW;
+  const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + h * 64;
+  const bf16* Kb = p.K + (int64_t)b * p.Tk * p.ldk + h * 64;
+  const bf16* Vb = p.V + (int64_t)b * p.Tk * p.ldv + h * 64;
+  const int off = p.Tk - p.Tq;   // causal diagonal offset
+
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) qf[qi][kk] = ld_frag(Qb, p.ldq, qw + qi * 16 + li, p.Tq, kk, lane);
+
+  f32x4 o[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) o[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {NEG_BIG, NEG_BIG}, l[2] = {0.f, 0.f};
+
+  int nkt = (p.Tk + KT - 1) / KT;
+  if (p.causal) {
+    const int qmax = min(p.Tq - 1, qblk + QB - 1);
+    const int kend = qmax + off + 1;
+    nkt = min(nkt, (kend + KT - 1) / KT);
+  }
+
+  auto stage = [&](int buf, int kt) {
+    char* Ks = smem + buf * 2 * TB;
+    const int k0 = kt * KT;
+    stage_tile(Kb + (int64_t)k0 * p.ldk, p.ldk, p.Tk - k0, Ks, wave, lane);
+    stage_tile(Vb + (int64_t)k0 * p.ldv, p.ldv, p.Tk - k0, Ks + TB, wave, lane);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    const char* Ks = smem + cur * 2 * TB;
+    const char* Vs = Ks + TB;
+    // S^T = K Q^T
+    f32x4 s[4][2];
+#pragma unroll
+    for (int kj = 0; kj < 4; ++kj) {
+      s[kj][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      s[kj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 kf = rd_row(Ks, kj * 16, kk, lane);
+        s[kj][0] = MFMA(kf, qf[0][kk], s[kj][0]);
+        s[kj][1] = MFMA(kf, qf[1][kk], s[kj][1]);
+      }
+    }
+    // online softmax (log2 domain), per query column
+    const int k0 = kt * KT;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      const int q = qw + qi * 16 + li;
+      float tmax = NEG_BIG;
+#pragma unroll
+      for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kj * 16 + 4 * g + r;
+          const bool ok = key < p.Tk && (!p.causal || key <= q + off);
+          const float x = ok ? s[kj][qi][r] * p.scale_log2 : -INFINITY;
+          s[kj][qi][r] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m[qi], tmax);
+      const float alpha = exp2f(m[qi] - mn);
+      m[qi] = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(s[kj][qi][r] - mn);
+          s[kj][qi][r] = e;
+          ls += e;
+        }
+      l[qi] = l[qi] * alpha + ls;
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) o[hj][qi] *= alpha;
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 p0 = pack8(s[2 * ss][0], s[2 * ss + 1][0]);
+      const bf16x8 p1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) {
+        const bf16x8 vf = rd_tr(Vs, hj * 16, ss, lane);
+        o[hj][0] = MFMA(vf, p0, o[hj][0]);
+        o[hj][1] = MFMA(vf, p1, o[hj][1]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    float lt = l[qi];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int q = qw + qi * 16 + li;
+    if (q < p.Tq) {
+      const float inv = 1.f / lt;
+      bf16* Ob = p.O + ((int64_t)b * p.Tq + q) * p.ldo + h * 64;
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) {
+        const f32x4 v = o[hj][qi] * inv;
+        *(bf16x4*)(Ob + hj * 16 + 4 * g) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      }
+      if (g == 0 && p.lse) p.lse[(int64_t)bh * p.Tq + q] = (m[qi] + log2f(lt)) / LOG2E;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// D[b,h,q] = sum_e dO[q][e] * O[q][e]     (one wave per (row, head))
+__global__ void attn_bwd_pre_kernel(const bf16* __restrict__ dO, int64_t lddo, const bf16* __restrict__ O,
+                                    int64_t ldo, float* __restrict__ Dv, int B, int H, int Tq) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= (int64_t)B * Tq * H) return;
+  const int lane = lane_id();
+  const int h = w % H;
+  const int64_t row = w / H;   // b*Tq + q
+  const float v = bf2f(dO[row * lddo + h * 64 + lane]) * bf2f(O[row * ldo + h * 64 + lane]);
+  const float s = wave_sum(v);
+  if (lane == 0) {
+    const int b = row / Tq, q = row % Tq;
+    Dv[((int64_t)b * H + h) * Tq + q] = s;
+  }
+}
+
+// dQ: per query block, loop over key tiles (K, V in LDS)
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+  const int lane = lane_id(), wave = wave_id_uniform();
+  const int g = lane >> 4, li = lane & 15;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int qblk = blockIdx.x * QB;
+  const int qw = qblk + wave * QW;
+  const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + h * 64;
+  const bf16* dOb = p.dO + (int64_t)b * p.Tq * p.lddo + h * 64;
+  const bf16* Kb = p.K + (int64_t)b * p.Tk * p.ldk + h * 64;
+  const bf16* Vb = p.V + (int64_t)b * p.Tk * p.ldv + h * 64;
+  const int off = p.Tk - p.Tq;
+
+  bf16x8 qf[2][2], dof[2][2];
+  float lse2[2], Dq[2];
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const int q = qw + qi * 16 + li;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[qi][kk] = ld_frag(Qb, p.ldq, q, p.Tq, kk, lane);
+      dof[qi][kk] = ld_frag(dOb, p.lddo, q, p.Tq, kk, lane);
+    }
+    lse2[qi] = q < p.Tq ? p.lse[(int64_t)bh * p.Tq + q] * LOG2E : 0.f;
+    Dq[qi] = q < p.Tq ? p.Dv[(int64_t)bh * p.Tq + q] : 0.f;
+  }
+  f32x4 dq[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dq[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int nkt = (p.Tk + KT - 1) / KT;
+  if (p.causal) {
+    const int qmax = min(p.Tq - 1, qblk + QB - 1);
+    nkt = min(nkt, (qmax + off + 1 + KT - 1) / KT);
+  }
+  auto stage = [&](int buf, int kt) {
+    char* Ks = smem + buf * 2 * TB;
+    const int k0 = kt * KT;
+    stage_tile(Kb + (int64_t)k0 * p.ldk, p.ldk, p.Tk - k0, Ks, wave, lane);
+    stage_tile(Vb + (int64_t)k0 * p.ldv, p.ldv, p.Tk - k0, Ks + TB, wave, lane);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    const char* Ks = smem + cur * 2 * TB;
+    const char* Vs = Ks + TB;
+    f32x4 s[4][2], dp[4][2];
+#pragma unroll
+    for (int kj = 0; kj < 4; ++kj) {
+      s[kj][0] = s[kj][1] = dp[kj][0] = dp[kj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 kf = rd_row(Ks, kj * 16, kk, lane);
+        const bf16x8 vf = rd_row(Vs, kj * 16, kk, lane);
+        s[kj][0] = MFMA(kf, qf[0][kk], s[kj][0]);
+        s[kj][1] = MFMA(kf, qf[1][kk], s[kj][1]);
+        dp[kj][0] = MFMA(vf, dof[0][kk], dp[kj][0]);
+        dp[kj][1] = MFMA(vf, dof[1][kk], dp[kj][1]);
+      }
+    }
+    const int k0 = kt * KT;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      const int q = qw + qi * 16 + li;
+#pragma unroll
+      for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kj * 16 + 4 * g + r;
+          const bool ok = key < p.Tk && q < p.Tq && (!p.causal || key <= q + off);
+          const float pr = ok ? exp2f(s[kj][qi][r] * p.scale_log2 - lse2[qi]) : 0.f;
+          s[kj][qi][r] = pr * (dp[kj][qi][r] - Dq[qi]);   // dS^T
+        }
+    }
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 d0 = pack8(s[2 * ss][0], s[2 * ss + 1][0]);
+      const bf16x8 d1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) {
+        const bf16x8 kt_ = rd_tr(Ks, hj * 16, ss, lane);
+        dq[hj][0] = MFMA(kt_, d0, dq[hj][0]);
+        dq[hj][1] = MFMA(kt_, d1, dq[hj][1]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const int q = qw + qi * 16 + li;
+    if (q < p.Tq) {
+      bf16* out = p.dQ + ((int64_t)b * p.Tq + q) * p.lddq + h * 64;
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) {
+        const f32x4 v = dq[hj][qi] * p.scale;
+        *(bf16x4*)(out + hj * 16 + 4 * g) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      }
+    }
+  }
+}
+
+// dK, dV: per key block (32 keys per wave, 128 per workgroup), loop over query tiles
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnP p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 2 * 2 * 64 * 4];
+  const int lane = lane_id(), wave = wave_id_uniform();
+  const int g = lane >> 4, li = lane & 15;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int kblk = blockIdx.x * QB;
+  const int kw = kblk + wave * QW;
+  const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + h * 64;
+  const bf16* dOb = p.dO + (int64_t)b * p.Tq * p.lddo + h * 64;
+  const bf16* Kb = p.K + (int64_t)b * p.Tk * p.ldk + h * 64;
+  const bf16* Vb = p.V + (int64_t)b * p.Tk * p.ldv + h * 64;
+  const int off = p.Tk - p.Tq;
+  float* rowc = (float*)(smem + 4 * TB);   // [2 stages][lse2 64 | D 64]
+
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int kj = 0; kj < 2; ++kj)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[kj][kk] = ld_frag(Kb, p.ldk, kw + kj * 16 + li, p.Tk, kk, lane);
+      vf[kj][kk] = ld_frag(Vb, p.ldv, kw + kj * 16 + li, p.Tk, kk, lane);
+    }
+  f32x4 dk[4][2], dv[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dk[i][j] = dv[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nqt_all = (p.Tq + KT - 1) / KT;
+  int qt0 = 0;
+  if (p.causal) {
+    const int qmin = kblk - off;   // first query that can see this key block
+    qt0 = qmin > 0 ? qmin / KT : 0;
+  }
+  auto stage = [&](int buf, int qt) {
+    char* Qs = smem + buf * 2 * TB;
+    const int q0 = qt * KT;
+    stage_tile(Qb + (int64_t)q0 * p.ldq, p.ldq, p.Tq - q0, Qs, wave, lane);
+    stage_tile(dOb + (int64_t)q0 * p.lddo, p.lddo, p.Tq - q0, Qs + TB, wave, lane);
+    if (threadIdx.x < 64) {
+      const int q = q0 + threadIdx.x;
+      rowc[buf * 128 + threadIdx.x] = q < p.Tq ? p.lse[(int64_t)bh * p.Tq + q] * LOG2E : 0.f;
+      rowc[buf * 128 + 64 + threadIdx.x] = q < p.Tq ? p.Dv[(int64_t)bh * p.Tq + q] : 0.f;
+    }
+  };
+  if (qt0 < nqt_all) {
+    stage(0, qt0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int qt = qt0; qt < nqt_all; ++qt) {
+    const int cur = (qt - qt0) & 1;
+    if (qt + 1 < nqt_all) stage(cur ^ 1, qt + 1);
+    const char* Qs = smem + cur * 2 * TB;
+    const char* dOs = Qs + TB;
+    const float* lrow = rowc + cur * 128;
+    const int q0 = qt * KT;
+    // S[q][key], dP[q][key] for 64 q x 32 keys
+    f32x4 s[4][2], dp[4][2];
+#pragma unroll
+    for (int qf = 0; qf < 4; ++qf) {
+      s[qf][0] = s[qf][1] = dp[qf][0] = dp[qf][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 qa = rd_row(Qs, qf * 16, kk, lane);
+        const bf16x8 da = rd_row(dOs, qf * 16, kk, lane);
+        s[qf][0] = MFMA(qa, kf[0][kk], s[qf][0]);
+        s[qf][1] = MFMA(qa, kf[1][kk], s[qf][1]);
+        dp[qf][0] = MFMA(da, vf[0][kk], dp[qf][0]);
+        dp[qf][1] = MFMA(da, vf[1][kk], dp[qf][1]);
+      }
+    }
+#pragma unroll
+    for (int qf = 0; qf < 4; ++qf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = qf * 16 + 4 * g + r;
+        const int q = q0 + ql;
+        const float l2 = lrow[ql], Dq = lrow[64 + ql];
+#pragma unroll
+        for (int kj = 0; kj < 2; ++kj) {
+          const int key = kw + kj * 16 + li;
+          const bool ok = q < p.Tq && key < p.Tk && (!p.causal || key <= q + off);
+          const float pr = ok ? exp2f(s[qf][kj][r] * p.scale_log2 - l2) : 0.f;
+          s[qf][kj][r] = pr;                              // P
+          dp[qf][kj][r] = pr * (dp[qf][kj][r] - Dq);      // dS
+        }
+      }
+    // dV^T += dO^T P ; dK^T += Q^T dS
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 p0 = pack8(s[2 * ss][0], s[2 * ss + 1][0]);
+      const bf16x8 p1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
+      const bf16x8 d0 = pack8(dp[2 * ss][0], dp[2 * ss + 1][0]);
+      const bf16x8 d1 = pack8(dp[2 * ss][1], dp[2 * ss + 1][1]);
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) {
+        const bf16x8 dot = rd_tr(dOs, hj * 16, ss, lane);
+        const bf16x8 qt_ = rd_tr(Qs, hj * 16, ss, lane);
+        dv[hj][0] = MFMA(dot, p0, dv[hj][0]);
+        dv[hj][1] = MFMA(dot, p1, dv[hj][1]);
+        dk[hj][0] = MFMA(qt_, d0, dk[hj][0]);
+        dk[hj][1] = MFMA(qt_, d1, dk[hj][1]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int kj = 0; kj < 2; ++kj) {
+    const int key = kw + kj * 16 + li;
+    if (key < p.Tk) {
+      bf16* ok_ = p.dK + ((int64_t)b * p.Tk + key) * p.lddk + h * 64;
+      bf16* ov_ = p.dV + ((int64_t)b * p.Tk + key) * p.lddv + h * 64;
+#pragma unroll
+      for (int hj = 0; hj < 4; ++hj) {
+        const f32x4 a = dk[hj][kj] * p.scale;
+        const f32x4 c = dv[hj][kj];
+        *(bf16x4*)(ok_ + hj * 16 + 4 * g) = bf16x4{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3])};
+        *(bf16x4*)(ov_ + hj * 16 + 4 * g) = bf16x4{f2bf(c[0]), f2bf(c[1]), f2bf(c[2]), f2bf(c[3])};
+      }
+    }
+  }
+}
+
+bool check_common(const void* Q, const void* K, const void* V, int64_t ldq, int64_t ldk, int64_t ldv) {
+  if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V) & 15) return false;
+  if ((ldq | ldk | ldv) & 7) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv, void* O,
+                           int64_t ldo, float* lse, int B, int H, int Tq, int Tk, int head_dim, int causal, float scale,
+                           hipStream_t stream) {
+  if (head_dim != 64) return TW_EUNSUPPORTED;
+  if (B <= 0 || Tq <= 0 || Tk <= 0) return TW_OK;
+  if (!check_common(Q, K, V, ldq, ldk, ldv) || (ldo & 3)) return TW_EINVAL;
+  if (causal && Tq > Tk) return TW_EINVAL;
+  AttnP p = {};
+  p.Q = (const bf16*)Q; p.K = (const bf16*)K; p.V = (const bf16*)V; p.O = (bf16*)O; p.lse = lse;
+  p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
+  p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
+  p.scale = scale; p.scale_log2 = scale * LOG2E;
+  dim3 grid((Tq + QB - 1) / QB, B * H);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, p);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+// workspace: B*H*Tq floats (the D = rowsum(dO*O) vector)
+extern "C" int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
+                           const void* O, int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ,
+                           int64_t lddq, void* dK, int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq, int Tk,
+                           int head_dim, int causal, float scale, float* workspace, hipStream_t stream) {
+  if (head_dim != 64) return TW_EUNSUPPORTED;
+  if (B <= 0 || Tq <= 0 || Tk <= 0) return TW_OK;
+  if (!check_common(Q, K, V, ldq, ldk, ldv) || ((uintptr_t)dO & 15) || (lddo & 7)) return TW_EINVAL;
+  if (causal && Tq > Tk) return TW_EINVAL;
+  AttnP p = {};
+  p.Q = (const bf16*)Q; p.K = (const bf16*)K; p.V = (const bf16*)V; p.lse = (float*)lse;
+  p.dO = (const bf16*)dO; p.Dv = workspace; p.dQ = (bf16*)dQ; p.dK = (bf16*)dK; p.dV = (bf16*)dV;
+  p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo; p.lddo = lddo; p.lddq = lddq; p.lddk = lddk; p.lddv = lddv;
+  p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
+  p.scale = scale; p.scale_log2 = scale * LOG2E;
+  const int64_t nw = (int64_t)B * Tq * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((nw + 3) / 4), dim3(256), 0, stream, (const bf16*)dO, lddo,
+                     (const bf16*)O, ldo, workspace, B, H, Tq);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Tk + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}

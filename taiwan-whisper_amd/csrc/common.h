@@ -1,0 +1,78 @@
+// Shared device helpers for the tw HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) void lds_void;
+
+// status codes of the C-ABI (include/tw_hip.h)
+#define TW_OK 0
+#define TW_EINVAL 1
+#define TW_EUNSUPPORTED 2
+#define TW_EHIP 3
+
+#define TW_CHECK_LAUNCH()                                   \
+  do {                                                      \
+    hipError_t e__ = hipGetLastError();                     \
+    if (e__ != hipSuccess) return TW_EHIP;                  \
+  } while (0)
+
+// dtype codes shared with the host side
+enum { TW_F32 = 0, TW_BF16 = 1 };
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+__device__ __forceinline__ float rbf(float x) { return (float)(bf16)x; }   // round-trip through bf16 (RNE)
+
+__device__ __forceinline__ float ld_as_f32(const void* p, int dtype, int64_t i) {
+  return dtype == TW_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {   // exact GELU (HF ACT2FN["gelu"])
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// raw buffer descriptor: out-of-range per-lane offsets (>= num_records) read as zero.
+#define TW_OOB 0x80000000u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0x80000000, 0x00020000);
+}
+
+// 16-byte buffer load straight into LDS: lane l writes lds_base + 16*l (wave-uniform base).
+__device__ __forceinline__ void buf_load_lds16(__amdgpu_buffer_rsrc_t r, void* lds_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id_uniform() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// order-preserving float <-> uint mapping for atomicMax on floats
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}

@@ -1,0 +1,258 @@
+// bf16 MFMA GEMM with fused epilogues (gfx950).
+//
+//   C[b][m][n] = epilogue( alpha * sum_k A[b][m][k] * B[b][n][k] )
+//
+// A is K-major ([M][K], lda) or MN-major ([K][M], lda) — template AT;
+// B is K-major ([N][K], ldb, the nn.Linear weight layout) or MN-major ([K][N]) — BT.
+// So one kernel serves forward (AT=0,BT=0: X·Wᵀ), dX (AT=0,BT=1: dY·W) and
+// dW (AT=1,BT=1: dYᵀ·X) of every Linear / conv-as-GEMM of the Whisper step
+// (SURVEY.md §2.2 K2/K4/K6/K8/K10).
+//
+// Tiling: 128x128x64 per 256-thread workgroup (2x2 waves of 64x64), v_mfma_f32_16x16x32_bf16,
+// operands staged HBM->LDS with buffer_load ... lds (16 B per lane, out-of-range lanes
+// read zero through the buffer descriptor), two LDS stages (64 KiB), one barrier per K-step.
+// K-major LDS images: 128-B rows, 16-B chunk c of row r at c ^ (r & 7) (ds_read_b128
+// conflict-free).  MN-major images: 256-B k-rows, 32-B slot s of k-row r at
+// s ^ ((r & 3) | ((r >> 3) & 1) << 2), read with ds_read_b64_tr_b16 (conflict-free).
+// The MFMA is issued with operands swapped (Bfrag, Afrag) so each lane ends up holding
+// 4 consecutive output columns of one row: 8/16-B stores in the epilogue.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;   // 16 KiB per operand per stage
+
+enum {
+  F_BIAS = 1,      // v += bias[n]            (bias bf16, autocast casts it)
+  F_ROUND = 2,     // v = bf16(v)             (autocast Linear output)
+  F_GELU = 4,      // [aux = v]; v = bf16(gelu(v))
+  F_RES = 8,       // v = res[m % res_mod][n] + v
+  F_ACCUM = 16,    // v += C_old
+  F_AUX_OUT = 32,  // store pre-activation to aux (with F_GELU)
+  F_DGELU = 64,    // v = bf16(v * gelu'(aux[m][n]))  (gelu backward, aux = pre-activation)
+};
+
+struct GemmP {
+  const bf16* A; const bf16* B; void* C;
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int64_t sA, sB, sC;
+  float alpha;
+  const bf16* bias;
+  const void* res; int64_t ldr; int64_t sR; int res_dtype; int res_mod;
+  bf16* aux; int64_t ldaux; int64_t sAux;
+  int c_dtype; int flags;
+};
+
+__device__ __forceinline__ int xr_mn(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+// K-major tile [128 rows][64 k] -> LDS (16 pieces of 1 KiB, 4 per wave)
+__device__ __forceinline__ void stage_k(const bf16* base, int64_t ld, int rows_left, int k_left,
+                                        char* lds, int wave, int lane) {
+  const auto rs = make_rsrc(base);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pce = wave + 4 * i;
+    const int r = pce * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const bool ok = (r < rows_left) && (c * 8 < k_left);
+    const uint32_t off = ok ? (uint32_t)(((int64_t)r * ld + c * 8) * 2) : TW_OOB;
+    buf_load_lds16(rs, lds + pce * 1024, off);
+  }
+}
+
+// MN-major tile [64 k-rows][128 cols] -> LDS (16 pieces of 4 k-rows)
+__device__ __forceinline__ void stage_mn(const bf16* base, int64_t ld, int cols_left, int k_left,
+                                         char* lds, int wave, int lane) {
+  const auto rs = make_rsrc(base);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pce = wave + 4 * i;
+    const int kr = pce * 4 + (lane >> 4);
+    const int pc = lane & 15;
+    const int s = (pc >> 1) ^ xr_mn(kr);
+    const int col = s * 16 + (pc & 1) * 8;
+    const bool ok = (kr < k_left) && (col < cols_left);
+    const uint32_t off = ok ? (uint32_t)(((int64_t)kr * ld + col) * 2) : TW_OOB;
+    buf_load_lds16(rs, lds + pce * 1024, off);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag_k(const char* tile, int rbase, int kk, int lane) {
+  const int r = rbase + (lane & 15);
+  const int c = kk * 4 + (lane >> 4);
+  return *(const bf16x8*)(tile + r * 128 + ((c ^ (r & 7)) << 4));
+}
+
+__device__ __forceinline__ bf16x8 frag_mn(const char* tile, int cbase, int kk, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int col = cbase + 4 * (i & 3);
+  const int slot = col >> 4, inoff = (col & 15) * 2;
+  const int kr0 = kk * 32 + 8 * g + (i >> 2);
+  const int kr1 = kr0 + 4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const char* a0 = tile + kr0 * 256 + ((slot ^ xr_mn(kr0)) << 5) + inoff;
+  const char* a1 = tile + kr1 * 256 + ((slot ^ xr_mn(kr1)) << 5) + inoff;
+  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a1);
+  s16x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  const int lane = lane_id();
+  const int wave = wave_id_uniform();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int bz = blockIdx.z;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+
+  const bf16* A = p.A + bz * p.sA;
+  const bf16* B = p.B + bz * p.sB;
+  const int K = p.K;
+  const int nk = (K + BK - 1) / BK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf, int kt) {
+    char* As = smem + buf * 2 * TILE_BYTES;
+    char* Bs = As + TILE_BYTES;
+    const int k0 = kt * BK;
+    if (AT) stage_mn(A + (int64_t)k0 * p.lda + m0, p.lda, p.M - m0, K - k0, As, wave, lane);
+    else    stage_k(A + (int64_t)m0 * p.lda + k0, p.lda, p.M - m0, K - k0, As, wave, lane);
+    if (BT) stage_mn(B + (int64_t)k0 * p.ldb + n0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
+    else    stage_k(B + (int64_t)n0 * p.ldb + k0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const char* As = smem + cur * 2 * TILE_BYTES;
+    const char* Bs = As + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+        a[mi] = AT ? frag_mn(As, wm * 64 + mi * 16, kk, lane) : frag_k(As, wm * 64 + mi * 16, kk, lane);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        b[ni] = BT ? frag_mn(Bs, wn * 64 + ni * 16, kk, lane) : frag_k(Bs, wn * 64 + ni * 16, kk, lane);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3] per fragment
+  const int g = lane >> 4, li = lane & 15;
+  const int flags = p.flags;
+  char* C = (char*)p.C;
+  const int esz = p.c_dtype == TW_BF16 ? 2 : 4;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + li;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wn * 64 + ni * 16 + 4 * g;
+      if (n >= p.N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[mi][ni][r];
+      const bool full = (n + 3 < p.N);
+      const int nv = full ? 4 : (p.N - n);
+      if (flags & F_BIAS) {
+        for (int r = 0; r < nv; ++r) v[r] += bf2f(p.bias[n + r]);
+      }
+      if (flags & F_ROUND) {
+        for (int r = 0; r < 4; ++r) v[r] = rbf(v[r]);
+      }
+      if (flags & F_DGELU) {
+        const bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
+        for (int r = 0; r < nv; ++r) v[r] = rbf(v[r] * gelu_erf_grad(bf2f(ax[r])));
+      }
+      if (flags & F_GELU) {
+        if (flags & F_AUX_OUT) {
+          bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
+          for (int r = 0; r < nv; ++r) ax[r] = f2bf(v[r]);
+        }
+        for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_erf(v[r]));
+      }
+      if (flags & F_RES) {
+        const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
+        const int64_t ro = bz * p.sR + (int64_t)mr * p.ldr + n;
+        for (int r = 0; r < nv; ++r) v[r] += ld_as_f32(p.res, p.res_dtype, ro + r);
+      }
+      const int64_t co = bz * p.sC + (int64_t)m * p.ldc + n;
+      if (flags & F_ACCUM) {
+        for (int r = 0; r < nv; ++r) v[r] += ld_as_f32(C, p.c_dtype, co + r);
+      }
+      if (p.c_dtype == TW_BF16) {
+        bf16* cp = (bf16*)C + co;
+        if (full && ((co & 3) == 0)) {
+          bf16x4 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          *(bf16x4*)cp = o;
+        } else {
+          for (int r = 0; r < nv; ++r) cp[r] = f2bf(v[r]);
+        }
+      } else {
+        float* cp = (float*)C + co;
+        if (full && ((co & 3) == 0)) {
+          *(f32x4*)cp = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          for (int r = 0; r < nv; ++r) cp[r] = v[r];
+        }
+      }
+    }
+  }
+  (void)esz;
+}
+
+}  // namespace
+
+extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
+                            void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
+                            int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
+                            const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
+                            void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return TW_OK;
+  if (K <= 0) return TW_EINVAL;
+  if ((!a_trans || !b_trans) && (K % 8) != 0) return TW_EINVAL;  // 16-B k-chunks of K-major operands
+  if (a_trans && (M % 8) != 0) return TW_EINVAL;                // 16-B column chunks
+  if (b_trans && (N % 8) != 0) return TW_EINVAL;
+  if ((lda % 8) != 0 || (ldb % 8) != 0) return TW_EINVAL;       // 16-B aligned rows / k-rows
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return TW_EINVAL;
+  if ((flags & F_BIAS) && !bias) return TW_EINVAL;
+  if ((flags & F_RES) && !res) return TW_EINVAL;
+  if ((flags & (F_AUX_OUT | F_DGELU)) && !aux) return TW_EINVAL;
+  if (c_dtype != TW_F32 && c_dtype != TW_BF16) return TW_EUNSUPPORTED;
+  GemmP p;
+  p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+  p.sA = sA; p.sB = sB; p.sC = sC; p.alpha = alpha; p.bias = (const bf16*)bias;
+  p.res = res; p.ldr = ldr; p.sR = sR; p.res_dtype = res_dtype; p.res_mod = res_mod;
+  p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux; p.c_dtype = c_dtype; p.flags = flags;
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
+  if (grid.y > 65535 || batch > 65535) return TW_EINVAL;
+  if (!a_trans && !b_trans) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NT), 0, stream, p);
+  else if (!a_trans && b_trans) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NT), 0, stream, p);
+  else if (a_trans && !b_trans) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NT), 0, stream, p);
+  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NT), 0, stream, p);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}

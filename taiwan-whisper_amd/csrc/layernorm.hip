@@ -1,0 +1,196 @@
+// LayerNorm forward/backward.  Rows of D elements, one wave per row,
+// fp32 statistics (autocast runs layer_norm in fp32: HF modeling_whisper.py:392,402,470,
+// 485,498,642,790).  Input fp32 (student residual stream) or bf16 (teacher stream);
+// output bf16 (feeds the next bf16 GEMM) or fp32.
+#include "common.h"
+
+namespace {
+
+constexpr int WPB = 4;   // waves (rows) per block
+
+template <int VEC, int MAXJ>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_dtype,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     void* __restrict__ y, int y_dtype, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int rows, int D, float eps) {
+  const int lane = lane_id();
+  const int row = blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int J = D / (64 * VEC);
+  const int64_t base = (int64_t)row * D;
+  float v[MAXJ][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j < J) {
+      const int e = (j * 64 + lane) * VEC;
+      if (VEC == 4) {
+        if (x_dtype == TW_F32) {
+          f32x4 t = *(const f32x4*)((const float*)x + base + e);
+          v[j][0] = t[0]; v[j][1] = t[1]; v[j][2] = t[2]; v[j][3] = t[3];
+        } else {
+          bf16x4 t = *(const bf16x4*)((const bf16*)x + base + e);
+          v[j][0] = bf2f(t[0]); v[j][1] = bf2f(t[1]); v[j][2] = bf2f(t[2]); v[j][3] = bf2f(t[3]);
+        }
+      } else {
+        v[j][0] = ld_as_f32(x, x_dtype, base + e);
+      }
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) s += v[j][q];
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j)
+    if (j < J)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) { const float d = v[j][q] - mean; ss += d * d; }
+  const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j < J) {
+      const int e = (j * 64 + lane) * VEC;
+      float o[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o[q] = (v[j][q] - mean) * rstd * w[e + q] + b[e + q];
+      if (y_dtype == TW_BF16) {
+        if (VEC == 4) *(bf16x4*)((bf16*)y + base + e) = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+        else ((bf16*)y)[base + e] = f2bf(o[0]);
+      } else {
+        if (VEC == 4) *(f32x4*)((float*)y + base + e) = f32x4{o[0], o[1], o[2], o[3]};
+        else ((float*)y)[base + e] = o[0];
+      }
+    }
+  }
+}
+
+// dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)); dx accumulated into dx_out (fp32).
+// Per-block partial dw/db written to partial[blockIdx.x][2][D] for a column reduction.
+template <int VEC, int MAXJ>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x, int x_dtype,
+                                                     const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const void* __restrict__ dy,
+                                                     int dy_dtype, float* __restrict__ dx, int dx_accum,
+                                                     float* __restrict__ partial, int rows, int D) {
+  __shared__ float red[WPB][2][1280];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const int J = D / (64 * VEC);
+  float dw[MAXJ][VEC], db[MAXJ][VEC];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) { dw[j][q] = 0.f; db[j][q] = 0.f; }
+  for (int row = blockIdx.x * WPB + wv; row < rows; row += gridDim.x * WPB) {
+    const int64_t base = (int64_t)row * D;
+    const float mu = mean_in[row], rs = rstd_in[row];
+    float xh[MAXJ][VEC], g[MAXJ][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (j < J) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const int e = (j * 64 + lane) * VEC + q;
+          const float xv = ld_as_f32(x, x_dtype, base + e);
+          const float dv = ld_as_f32(dy, dy_dtype, base + e);
+          xh[j][q] = (xv - mu) * rs;
+          g[j][q] = dv * w[e];
+          s1 += g[j][q];
+          s2 += g[j][q] * xh[j][q];
+          dw[j][q] += dv * xh[j][q];
+          db[j][q] += dv;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (j < J) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const int e = (j * 64 + lane) * VEC + q;
+          const float o = rs * (g[j][q] - s1 - xh[j][q] * s2);
+          if (dx_accum) dx[base + e] += o; else dx[base + e] = o;
+        }
+      }
+    }
+  }
+  // block reduction of dw/db over the 4 waves
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j)
+    if (j < J)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        const int e = (j * 64 + lane) * VEC + q;
+        red[wv][0][e] = dw[j][q];
+        red[wv][1][e] = db[j][q];
+      }
+  __syncthreads();
+  for (int e = threadIdx.x; e < D; e += blockDim.x) {
+    float a = 0.f, c = 0.f;
+#pragma unroll
+    for (int k = 0; k < WPB; ++k) { a += red[k][0][e]; c += red[k][1][e]; }
+    partial[(int64_t)blockIdx.x * 2 * D + e] = a;
+    partial[(int64_t)blockIdx.x * 2 * D + D + e] = c;
+  }
+}
+
+// dw_out[c] += sum_b partial[b][0][c]; db_out[c] += sum_b partial[b][1][c]
+__global__ void ln_param_reduce_kernel(const float* __restrict__ partial, int nb, int D, float* __restrict__ dw_out,
+                                       float* __restrict__ db_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float a = 0.f, s = 0.f;
+  for (int b = 0; b < nb; ++b) {
+    a += partial[(int64_t)b * 2 * D + c];
+    s += partial[(int64_t)b * 2 * D + D + c];
+  }
+  if (dw_out) dw_out[c] += a;
+  if (db_out) db_out[c] += s;
+}
+
+}  // namespace
+
+extern "C" int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, const float* b, void* y, int y_dtype,
+                                float* mean_out, float* rstd_out, int rows, int D, float eps, hipStream_t stream) {
+  if (rows <= 0) return TW_OK;
+  if (D % 64 || D > 1280) return TW_EUNSUPPORTED;
+  dim3 grid((rows + WPB - 1) / WPB), block(64 * WPB);
+  if (D % 256 == 0)
+    hipLaunchKernelGGL((ln_fwd_kernel<4, 5>), grid, block, 0, stream, x, x_dtype, w, b, y, y_dtype, mean_out,
+                       rstd_out, rows, D, eps);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<1, 20>), grid, block, 0, stream, x, x_dtype, w, b, y, y_dtype, mean_out,
+                       rstd_out, rows, D, eps);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+// workspace: >= nblk*2*D floats where nblk = min(1024, ceil(rows/4)); dw/db accumulated into dw_out/db_out
+extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd,
+                                const void* dy, int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out,
+                                int rows, int D, float* workspace, int64_t workspace_floats, hipStream_t stream) {
+  if (rows <= 0) return TW_OK;
+  if (D % 64 || D > 1280) return TW_EUNSUPPORTED;
+  int nblk = (rows + WPB - 1) / WPB;
+  if (nblk > 1024) nblk = 1024;
+  if (workspace_floats < (int64_t)nblk * 2 * D) return TW_EINVAL;
+  if (D % 256 == 0)
+    hipLaunchKernelGGL((ln_bwd_kernel<4, 5>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy, dy_dtype,
+                       dx, dx_accum, workspace, rows, D);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<1, 20>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy,
+                       dy_dtype, dx, dx_accum, workspace, rows, D);
+  TW_CHECK_LAUNCH();
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((D + 255) / 256), dim3(256), 0, stream, workspace, nblk, D, dw_out,
+                     db_out);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}

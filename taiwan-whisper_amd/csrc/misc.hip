@@ -1,0 +1,295 @@
+// HBM-bound helper kernels of the distillation step:
+//   embedding gather (+learned positions) and its scatter-add backward (K7),
+//   fp32->bf16 weight casts (autocast's per-forward weight cast), bias-grad column sums,
+//   global grad L2 norm + fused clip/AdamW update (K11/K12, run_distillation.py:1666-1668),
+//   conv-stem im2col / col2im for the conv backward (K2), teacher decoder-input shift
+//   (HF shift_tokens_right, run_distillation.py:1534) and valid-label count.
+#include "common.h"
+
+namespace {
+
+__global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const void* __restrict__ tok, int tok_dtype,
+                                 const void* __restrict__ pos, int pos_dtype, void* __restrict__ out, int out_dtype,
+                                 int rows, int T, int pos_offset, int D) {
+  const int row = blockIdx.x;
+  if (row >= rows) return;
+  const int64_t id = ids[row];
+  const int t = row % T + pos_offset;
+  for (int e = threadIdx.x; e < D; e += blockDim.x) {
+    const float a = ld_as_f32(tok, tok_dtype, id * D + e);
+    const float b = ld_as_f32(pos, pos_dtype, (int64_t)t * D + e);
+    const float s = a + b;
+    if (out_dtype == TW_BF16) ((bf16*)out)[(int64_t)row * D + e] = f2bf(s);
+    else ((float*)out)[(int64_t)row * D + e] = s;
+  }
+}
+
+__global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ dh, float* __restrict__ dE,
+                                 int rows, int D) {
+  const int row = blockIdx.x;
+  if (row >= rows) return;
+  const int64_t id = ids[row];
+  for (int e = threadIdx.x; e < D; e += blockDim.x) {
+    const float g = dh[(int64_t)row * D + e];
+    if (g != 0.f) atomicAdd(&dE[id * D + e], g);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int64_t n) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (; i + 3 < n; i += stride) {
+    f32x4 v = *(const f32x4*)(src + i);
+    *(bf16x4*)(dst + i) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  }
+  for (; i < n; ++i) dst[i] = f2bf(src[i]);
+}
+
+// out[c] (+)= bf16?(sum_r x[r][c]) : bias gradient of an autocast Linear (grad computed in bf16)
+__global__ void colsum_rows_kernel(const void* __restrict__ x, int x_dtype, int64_t ldx, int rows, int cols,
+                                   float* __restrict__ out, int accum, int round_bf16) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < cols)
+    for (int r = part; r < rows; r += 4) s += ld_as_f32(x, x_dtype, (int64_t)r * ldx + c);
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && c < cols) {
+    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (round_bf16) t = rbf(t);
+    out[c] = accum ? out[c] + t : t;
+  }
+}
+
+// sum of squares of a fp32 vector -> partial[blockIdx.x]
+__global__ void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void finalize_norm_kernel(const float* __restrict__ partial, int nb, float* __restrict__ norm_out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 64) s += partial[i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) norm_out[0] = sqrtf(s);
+}
+
+// torch.optim.AdamW (foreach=False, non-capturable) with the clip_grad_norm_ factor fused:
+//   g *= min(1, max_norm / (norm + 1e-6)); p *= 1 - lr*wd; m = lerp(m, g, 1-b1);
+//   v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps);  optional bf16 copy of p.
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, bf16* __restrict__ p_bf16, int64_t n, float lr, float b1, float b2,
+                             float eps, float wd, float bc1, float bc2_sqrt, const float* __restrict__ norm,
+                             float max_norm) {
+  float coef = 1.f;
+  if (norm != nullptr && max_norm > 0.f) {
+    coef = max_norm / (norm[0] + 1e-6f);
+    coef = coef < 1.f ? coef : 1.f;
+  }
+  const float step_size = lr / bc1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * coef;
+    float pi = p[i];
+    pi = pi * (1.f - lr * wd);
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+    if (p_bf16) p_bf16[i] = f2bf(pi);
+  }
+}
+
+__global__ void scale_kernel(float* __restrict__ x, int64_t n, const float* __restrict__ norm, float max_norm) {
+  float coef = max_norm / (norm[0] + 1e-6f);
+  if (coef >= 1.f) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] *= coef;
+}
+
+// dst[b*T_out + t][k*C + c] = src[b][t*stride + k][c]    (src rows per batch = src_rows)
+__global__ void im2col_kernel(const bf16* __restrict__ src, int64_t src_rows, bf16* __restrict__ dst, int B, int T_out,
+                              int stride, int C) {
+  const int64_t row = blockIdx.x;    // b*T_out + t
+  if (row >= (int64_t)B * T_out) return;
+  const int b = row / T_out, t = row % T_out;
+  for (int j = threadIdx.x; j < 3 * C; j += blockDim.x) {
+    const int k = j / C, c = j % C;
+    dst[row * 3 * C + j] = src[((int64_t)b * src_rows + (int64_t)t * stride + k) * C + c];
+  }
+}
+
+// conv2 (k3, s2, p1) input-gradient: dX[b][s][c] = sum over (t,k) with 2t+k-1 = s of dA[b*T_out+t][k*C+c]
+__global__ void col2im_s2_kernel(const float* __restrict__ dA, float* __restrict__ dX, int B, int T_in, int T_out,
+                                 int C) {
+  const int64_t row = blockIdx.x;    // b*T_in + s
+  if (row >= (int64_t)B * T_in) return;
+  const int b = row / T_in, s = row % T_in;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    if ((s & 1) == 0) {
+      const int t = s / 2;
+      acc = dA[((int64_t)b * T_out + t) * 3 * C + 1 * C + c];
+    } else {
+      const int t0 = (s + 1) / 2, t2 = (s - 1) / 2;
+      if (t0 < T_out) acc += dA[((int64_t)b * T_out + t0) * 3 * C + 0 * C + c];
+      acc += dA[((int64_t)b * T_out + t2) * 3 * C + 2 * C + c];
+    }
+    dX[row * C + c] = acc;
+  }
+}
+
+// HF shift_tokens_right on device: out[b][0] = start; out[b][t] = labels[b][t-1] (-100 -> pad)
+__global__ void shift_right_kernel(const int64_t* __restrict__ labels, int64_t* __restrict__ out, int B, int T,
+                                   int64_t pad, int64_t start) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * T) return;
+  const int t = i % T;
+  int64_t v = t == 0 ? start : labels[i - 1];
+  out[i] = v == -100 ? pad : v;
+}
+
+__global__ void count_valid_kernel(const int64_t* __restrict__ labels, int64_t n, int* __restrict__ out) {
+  int c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += labels[i] >= 0 ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+// mel [B][80][3000] f32 -> time-major bf16 conv1 input [B][3002][80] with zero rows 0 and 3001
+__global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, bf16* __restrict__ xt, int B, int nmel,
+                                         int T) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)B * (T + 2) * nmel;
+  if (i >= n) return;
+  const int c = i % nmel;
+  const int64_t r = i / nmel;
+  const int b = r / (T + 2), tt = r % (T + 2);
+  float v = 0.f;
+  if (tt >= 1 && tt <= T) v = mel[((int64_t)b * nmel + c) * T + (tt - 1)];
+  xt[i] = f2bf(v);
+}
+
+inline int nblocks(int64_t n, int bs, int cap = 4096) {
+  int64_t b = (n + bs - 1) / bs;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int tw_embed_fwd(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype,
+                            void* out, int out_dtype, int rows, int T, int pos_offset, int D, hipStream_t stream) {
+  if (rows <= 0) return TW_OK;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(rows), dim3(256), 0, stream, ids, tok, tok_dtype, pos, pos_dtype, out,
+                     out_dtype, rows, T, pos_offset, D);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D, hipStream_t stream) {
+  if (rows <= 0) return TW_OK;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(rows), dim3(256), 0, stream, ids, dh, dE, rows, D);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(nblocks(n / 4 + 1, 256)), dim3(256), 0, stream, src, (bf16*)dst, n);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum,
+                         int round_bf16, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0) return TW_OK;
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3((cols + 63) / 64), dim3(256), 0, stream, x, x_dtype, ldx, rows, cols,
+                     out, accum, round_bf16);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+// norm_out[0] = ||x||_2 ; workspace >= 1024 floats
+extern "C" int tw_l2norm(const float* x, int64_t n, float* norm_out, float* workspace, hipStream_t stream) {
+  const int nb = nblocks(n, 256, 1024);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, stream, x, n, workspace);
+  hipLaunchKernelGGL(finalize_norm_kernel, dim3(1), dim3(64), 0, stream, workspace, nb, norm_out);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float b1,
+                        float b2, float eps, float wd, int step, const float* norm, float max_norm,
+                        hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  if (step < 1) return TW_EINVAL;
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, p, g, m, v, (bf16*)p_bf16, n, lr,
+                     b1, b2, eps, wd, bc1, sqrtf(bc2), norm, max_norm);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_clip_scale(float* x, int64_t n, const float* norm, float max_norm, hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(scale_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, x, n, norm, max_norm);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_im2col3(const void* src, int64_t src_rows, void* dst, int B, int T_out, int stride, int C,
+                          hipStream_t stream) {
+  if (B <= 0 || T_out <= 0) return TW_OK;
+  hipLaunchKernelGGL(im2col_kernel, dim3((int64_t)B * T_out), dim3(256), 0, stream, (const bf16*)src, src_rows,
+                     (bf16*)dst, B, T_out, stride, C);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_col2im_s2(const float* dA, float* dX, int B, int T_in, int T_out, int C, hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  hipLaunchKernelGGL(col2im_s2_kernel, dim3((int64_t)B * T_in), dim3(256), 0, stream, dA, dX, B, T_in, T_out, C);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_shift_tokens_right(const int64_t* labels, int64_t* out, int B, int T, int64_t pad, int64_t start,
+                                     hipStream_t stream) {
+  const int64_t n = (int64_t)B * T;
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(shift_right_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, labels, out, B, T, pad, start);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_count_valid(const int64_t* labels, int64_t n, int* out, hipStream_t stream) {
+  if (hipMemsetAsync(out, 0, sizeof(int), stream) != hipSuccess) return TW_EHIP;
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(count_valid_kernel, dim3(nblocks(n, 256, 1024)), dim3(256), 0, stream, labels, n, out);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_mel_to_conv_input(const float* mel, void* xt, int B, int nmel, int T, hipStream_t stream) {
+  const int64_t n = (int64_t)B * (T + 2) * nmel;
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(mel_to_conv_input_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, mel, (bf16*)xt, B, nmel,
+                     T);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}

@@ -1,0 +1,227 @@
+"""Typed host wrappers over libtw_hip.so.
+
+Every wrapper validates dtypes, devices, alignment and — before any launch — that each
+operand's storage really holds every element the kernel will touch, so a wrong shape
+raises here instead of faulting the GPU.  All launches go on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._native import call
+
+F32, BF16 = 0, 1
+GEMM_BIAS, GEMM_ROUND, GEMM_GELU, GEMM_RES, GEMM_ACCUM, GEMM_AUX_OUT, GEMM_DGELU = 1, 2, 4, 8, 16, 32, 64
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"tw: unsupported dtype {t.dtype}")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _need(t: torch.Tensor, n_elems: int, what: str):
+    """Storage behind t (from t's first element) must hold n_elems elements."""
+    if t is None:
+        raise ValueError(f"tw: {what} is required")
+    if not t.is_cuda:
+        raise ValueError(f"tw: {what} must be a device tensor")
+    st = t.untyped_storage()
+    avail = (st.data_ptr() + st.nbytes() - t.data_ptr()) // t.element_size()
+    if n_elems > avail:
+        raise ValueError(f"tw: {what} needs {n_elems} elements past its start, storage has {avail}")
+
+
+def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, bias=None, res=None,
+         ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0):
+    """C[b] = epi(alpha * A[b] @ B[b]^T); A bf16 [M][K] (a_trans: [K][M]); B bf16 [N][K] (b_trans: [K][N])."""
+    if M <= 0 or N <= 0:
+        return C
+    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "tw.gemm: A and B must be bf16"
+    _need(A, (batch - 1) * sA + ((K - 1) * lda + M if a_trans else (M - 1) * lda + K), "gemm A")
+    _need(B, (batch - 1) * sB + ((K - 1) * ldb + N if b_trans else (N - 1) * ldb + K), "gemm B")
+    _need(C, (batch - 1) * sC + (M - 1) * ldc + N, "gemm C")
+    if bias is not None:
+        assert bias.dtype == torch.bfloat16
+        _need(bias, N, "gemm bias")
+        flags |= GEMM_BIAS
+    if res is not None:
+        rows = res_mod if res_mod > 0 else M
+        _need(res, (batch - 1) * sR + (rows - 1) * ldr + N, "gemm residual")
+        flags |= GEMM_RES
+    if aux is not None:
+        assert aux.dtype == torch.bfloat16
+        _need(aux, (batch - 1) * sAux + (M - 1) * ldaux + N, "gemm aux")
+    call("tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
+         M, N, K, batch, sA, sB, sC, float(alpha), _ptr(bias), _ptr(res), ldr, sR,
+         _dt(res) if res is not None else F32, res_mod, _ptr(aux), ldaux, sAux, flags, _stream())
+    return C
+
+
+def layernorm_fwd(x, w, b, y, mean=None, rstd=None, eps=1e-5):
+    D = x.shape[-1]
+    rows = x.numel() // D
+    assert x.is_contiguous() and y.is_contiguous() and y.numel() == x.numel()
+    assert w.dtype == torch.float32 and b.dtype == torch.float32 and w.numel() == D and b.numel() == D
+    if mean is not None:
+        _need(mean, rows, "ln mean"); _need(rstd, rows, "ln rstd")
+    call("tw_layernorm_fwd", x.data_ptr(), _dt(x), w.data_ptr(), b.data_ptr(), y.data_ptr(), _dt(y),
+         _ptr(mean), _ptr(rstd), rows, D, float(eps), _stream())
+    return y
+
+
+def layernorm_bwd(x, w, mean, rstd, dy, dx, dw, db, dx_accum=True, workspace=None):
+    D = x.shape[-1]
+    rows = x.numel() // D
+    assert dx.dtype == torch.float32 and dx.numel() == x.numel() and dy.numel() == x.numel()
+    nblk = min(1024, (rows + 3) // 4)
+    if workspace is None or workspace.numel() < nblk * 2 * D:
+        workspace = torch.empty(nblk * 2 * D, dtype=torch.float32, device=x.device)
+    call("tw_layernorm_bwd", x.data_ptr(), _dt(x), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
+         _dt(dy), dx.data_ptr(), int(dx_accum), _ptr(dw), _ptr(db), rows, D, workspace.data_ptr(),
+         workspace.numel(), _stream())
+    return dx
+
+
+def attn_fwd(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale):
+    hd = 64
+    for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o")):
+        assert t.dtype == torch.bfloat16
+        _need(t, (B * T - 1) * ld + H * hd, f"attn {nm}")
+    if lse is not None:
+        _need(lse, B * H * Tq, "attn lse")
+    call("tw_attn_fwd", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, _ptr(lse),
+         B, H, Tq, Tk, hd, int(causal), float(scale), _stream())
+    return o
+
+
+def attn_bwd(q, ldq, k, ldk, v, ldv, o, ldo, do, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Tq, Tk, causal,
+             scale, workspace=None):
+    hd = 64
+    for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o"),
+                         (do, lddo, Tq, "do"), (dq, lddq, Tq, "dq"), (dk, lddk, Tk, "dk"), (dv, lddv, Tk, "dv")):
+        assert t.dtype == torch.bfloat16, nm
+        _need(t, (B * T - 1) * ld + H * hd, f"attn_bwd {nm}")
+    _need(lse, B * H * Tq, "attn lse")
+    if workspace is None or workspace.numel() < B * H * Tq:
+        workspace = torch.empty(B * H * Tq, dtype=torch.float32, device=q.device)
+    call("tw_attn_bwd", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, do.data_ptr(),
+         lddo, lse.data_ptr(), dq.data_ptr(), lddq, dk.data_ptr(), lddk, dv.data_ptr(), lddv, B, H, Tq, Tk, hd,
+         int(causal), float(scale), workspace.data_ptr(), _stream())
+
+
+def kl_ce(s_logits, t_logits, labels, V, n_valid, T=2.0, ce_w=0.8, kl_w=1.0, grad_scale=1.0, dlogits=None,
+          row_out=None, out3=None):
+    rows, ld = s_logits.shape
+    assert t_logits.shape == s_logits.shape and s_logits.dtype == torch.bfloat16 and t_logits.dtype == torch.bfloat16
+    assert labels.dtype == torch.int64 and labels.numel() == rows and n_valid.dtype == torch.int32
+    if row_out is None:
+        row_out = torch.empty(rows * 2, dtype=torch.float32, device=s_logits.device)
+    if out3 is None:
+        out3 = torch.empty(3, dtype=torch.float32, device=s_logits.device)
+    if dlogits is not None:
+        assert dlogits.shape == s_logits.shape and dlogits.dtype == torch.bfloat16
+    call("tw_kl_ce", s_logits.data_ptr(), t_logits.data_ptr(), ld, labels.data_ptr(), rows, V, float(T),
+         float(ce_w), float(kl_w), n_valid.data_ptr(), float(grad_scale), row_out.data_ptr(), out3.data_ptr(),
+         _ptr(dlogits), _stream())
+    return out3, row_out
+
+
+def logmel(wav, basis, mel_start, mel_w, mel_out, conv_in=None, workspace=None):
+    B = wav.shape[0]
+    assert wav.shape == (B, 480000) and wav.dtype == torch.float32 and wav.is_contiguous()
+    assert mel_out.shape == (B, 80, 3000) and mel_out.dtype == torch.float32
+    if conv_in is not None:
+        assert conv_in.shape == (B, 3002, 80) and conv_in.dtype == torch.bfloat16
+    if workspace is None:
+        workspace = torch.empty(B, dtype=torch.int32, device=wav.device)
+    call("tw_logmel", wav.data_ptr(), B, basis.data_ptr(), mel_start.data_ptr(), mel_w.data_ptr(),
+         mel_out.data_ptr(), _ptr(conv_in), workspace.data_ptr(), _stream())
+    return mel_out
+
+
+def mel_to_conv_input(mel, xt):
+    B, nmel, T = mel.shape
+    assert xt.shape == (B, T + 2, nmel) and xt.dtype == torch.bfloat16 and mel.is_contiguous()
+    call("tw_mel_to_conv_input", mel.data_ptr(), xt.data_ptr(), B, nmel, T, _stream())
+    return xt
+
+
+def embed_fwd(ids, tok, pos, out, T, pos_offset=0):
+    rows = ids.numel()
+    D = tok.shape[1]
+    assert ids.dtype == torch.int64 and out.shape[-1] == D and out.numel() == rows * D
+    assert pos.shape[0] >= T + pos_offset
+    call("tw_embed_fwd", ids.data_ptr(), tok.data_ptr(), _dt(tok), pos.data_ptr(), _dt(pos), out.data_ptr(),
+         _dt(out), rows, T, pos_offset, D, _stream())
+    return out
+
+
+def embed_bwd(ids, dh, dE):
+    rows = ids.numel()
+    D = dE.shape[1]
+    assert dh.dtype == torch.float32 and dE.dtype == torch.float32 and dh.numel() == rows * D
+    call("tw_embed_bwd", ids.data_ptr(), dh.data_ptr(), dE.data_ptr(), rows, D, _stream())
+
+
+def cast_bf16(src, dst):
+    assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() <= dst.numel()
+    assert src.is_contiguous() and dst.is_contiguous()
+    call("tw_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), _stream())
+    return dst
+
+
+def colsum(x, ldx, rows, cols, out, accum=True, round_bf16=True):
+    _need(x, (rows - 1) * ldx + cols, "colsum x")
+    assert out.dtype == torch.float32 and out.numel() >= cols
+    call("tw_colsum", x.data_ptr(), _dt(x), ldx, rows, cols, out.data_ptr(), int(accum), int(round_bf16), _stream())
+
+
+def l2norm(x, out, workspace):
+    assert x.dtype == torch.float32 and x.is_contiguous() and workspace.numel() >= 1024
+    call("tw_l2norm", x.data_ptr(), x.numel(), out.data_ptr(), workspace.data_ptr(), _stream())
+    return out
+
+
+def adamw(p, g, m, v, p_bf16, lr, b1, b2, eps, wd, step, norm=None, max_norm=0.0):
+    n = p.numel()
+    assert g.numel() == n and m.numel() == n and v.numel() == n
+    if p_bf16 is not None:
+        assert p_bf16.numel() >= n and p_bf16.dtype == torch.bfloat16
+    call("tw_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(p_bf16), n, float(lr), float(b1),
+         float(b2), float(eps), float(wd), int(step), _ptr(norm), float(max_norm), _stream())
+
+
+def im2col3(src, src_rows, dst, B, T_out, stride, C):
+    _need(src, (B - 1) * src_rows * C + ((T_out - 1) * stride + 3) * C, "im2col src")
+    _need(dst, B * T_out * 3 * C, "im2col dst")
+    call("tw_im2col3", src.data_ptr(), src_rows, dst.data_ptr(), B, T_out, stride, C, _stream())
+
+
+def col2im_s2(dA, dX, B, T_in, T_out, C):
+    assert dA.dtype == torch.float32 and dX.dtype == torch.float32
+    _need(dA, B * T_out * 3 * C, "col2im dA"); _need(dX, B * T_in * C, "col2im dX")
+    call("tw_col2im_s2", dA.data_ptr(), dX.data_ptr(), B, T_in, T_out, C, _stream())
+
+
+def shift_tokens_right(labels, out, pad, start):
+    B, T = labels.shape
+    assert labels.dtype == torch.int64 and out.shape == labels.shape and labels.is_contiguous()
+    call("tw_shift_tokens_right", labels.data_ptr(), out.data_ptr(), B, T, pad, start, _stream())
+    return out
+
+
+def count_valid(labels, out):
+    assert labels.dtype == torch.int64 and out.dtype == torch.int32
+    call("tw_count_valid", labels.data_ptr(), labels.numel(), out.data_ptr(), _stream())
+    return out

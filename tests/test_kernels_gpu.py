@@ -1,0 +1,273 @@
+"""Per-kernel parity on the GPU: every HIP kernel vs an fp32 torch / oracle reference on
+the same (bf16-rounded) inputs.  Tolerances are stated per test: bf16 outputs are allowed
+~1 bf16 ulp (2^-8 relative) of rounding difference; fp32 outputs of MFMA GEMMs differ from
+the fp64 reference only by accumulation order."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from tw import _native
+    _native.lib()
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / max(b.abs().max().item(), 1e-30))
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(200, 136, 72), (128, 128, 64), (257, 520, 1280), (96, 51, 240)])
+def test_gemm_layouts(a_t, b_t, M, N, K):
+    from tw import ops
+    if (a_t and M % 8) or (b_t and N % 8):
+        pytest.skip("MN-major operands need 8-aligned extents")
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(N, K, generator=g)
+    ref = bf(A).double() @ bf(Bm).double().T
+    Ad = bf(A.T.contiguous() if a_t else A).to(DEV)
+    Bd = bf(Bm.T.contiguous() if b_t else Bm).to(DEV)
+    C = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(Ad, Bd, C, M, N, K, lda=M if a_t else K, ldb=N if b_t else K, ldc=N, a_trans=bool(a_t),
+             b_trans=bool(b_t))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 1e-5
+
+
+def test_gemm_epilogues():
+    from tw import ops
+    g = torch.Generator().manual_seed(1)
+    M, N, K, R = 300, 264, 128, 100
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.1
+    bias, res = torch.randn(N, generator=g), torch.randn(R, N, generator=g)
+    Ad, Wd, bd, rd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV), res.to(DEV)
+    acc = bf(A).double() @ bf(W).double().T
+    y = (acc + bf(bias).double()).float()
+    yb = bf(y).float()
+    # bias + round + gelu (aux = pre-activation) -> bf16
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, aux=aux, ldaux=N,
+             flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT)
+    gel = bf(torch.nn.functional.gelu(yb)).float()
+    assert (aux.float().cpu() - yb).abs().max() <= 2 ** -7 * yb.abs().max()
+    assert (C.float().cpu() - gel).abs().max() <= 2 ** -7 * gel.abs().max()
+    # residual broadcast with res_mod + fp32 out
+    C2 = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(Ad, Wd, C2, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rd, ldr=N, res_mod=R, flags=ops.GEMM_ROUND)
+    ref2 = yb + res[torch.arange(M) % R]
+    assert (C2.cpu() - ref2).abs().max() <= 2 ** -7 * yb.abs().max() + 1e-6
+    # accumulate
+    C3 = torch.ones(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(Ad, Wd, C3, M, N, K, lda=K, ldb=K, ldc=N, alpha=0.5, flags=ops.GEMM_ACCUM)
+    assert rel_err(C3 - 1.0, 0.5 * acc) < 1e-5
+    # dgelu: v = bf16(bf16(acc) * gelu'(aux))
+    C4 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(Ad, Wd, C4, M, N, K, lda=K, ldb=K, ldc=N, aux=aux, ldaux=N, flags=ops.GEMM_ROUND | ops.GEMM_DGELU)
+    x = aux.float().cpu().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(bf(acc.float()).float())
+    assert (C4.float().cpu() - x.grad).abs().max() <= 2 ** -7 * x.grad.abs().max() + 1e-6
+
+
+def test_gemm_batched_strided_view():
+    """conv2-style zero-copy im2col: A rows = 3 consecutive rows of a padded buffer (lda = 2*C)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(2)
+    B, Tin, C, Cout = 3, 40, 64, 72
+    x = torch.randn(B, Tin, C, generator=g)
+    w = torch.randn(Cout, C, 3, generator=g) * 0.1
+    ref = torch.nn.functional.conv1d(bf(x).float().transpose(1, 2), bf(w).float(), stride=2, padding=1)
+    ref = ref.transpose(1, 2)  # [B, Tout, Cout]
+    Tout = Tin // 2
+    H = torch.zeros(B, Tin + 2, C, dtype=torch.bfloat16)   # zero row in front (+1 spare)
+    H[:, 1:Tin + 1] = bf(x)
+    Hd = H.to(DEV)
+    Wk = bf(w.permute(0, 2, 1).reshape(Cout, 3 * C)).to(DEV)   # [Cout][k*C + c]
+    out = torch.empty(B, Tout, Cout, dtype=torch.float32, device=DEV)
+    ops.gemm(Hd, Wk, out, Tout, Cout, 3 * C, lda=2 * C, ldb=3 * C, ldc=Cout, batch=B, sA=(Tin + 2) * C, sB=0,
+             sC=Tout * Cout)
+    assert rel_err(out, ref) < 1e-5
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [64, 384, 1280])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_layernorm(D, xdt):
+    from tw import ops
+    g = torch.Generator().manual_seed(D)
+    rows = 333
+    x = (torch.randn(rows, D, generator=g) * 3 + 1).to(xdt)
+    w, b = torch.randn(D, generator=g), torch.randn(D, generator=g)
+    ref = torch.nn.functional.layer_norm(x.float(), (D,), w, b, 1e-5)
+    xd = x.to(DEV)
+    y = torch.empty(rows, D, dtype=torch.float32, device=DEV)
+    mean = torch.empty(rows, device=DEV); rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(xd, w.to(DEV), b.to(DEV), y, mean, rstd)
+    assert (y.cpu() - ref).abs().max() < 2e-5 * ref.abs().max()
+    yb = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    ops.layernorm_fwd(xd, w.to(DEV), b.to(DEV), yb)
+    assert (yb.float().cpu() - ref).abs().max() <= 2 ** -8 * ref.abs().max()
+    # backward
+    dy = torch.randn(rows, D, generator=g)
+    xr = x.float().requires_grad_(True); wr = w.clone().requires_grad_(True); br = b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5).backward(dy)
+    dx = torch.full((rows, D), 0.5, device=DEV)
+    dw = torch.zeros(D, device=DEV); db = torch.zeros(D, device=DEV)
+    ops.layernorm_bwd(xd, w.to(DEV), mean, rstd, dy.to(DEV), dx, dw, db, dx_accum=True)
+    assert rel_err(dx.cpu() - 0.5, xr.grad) < 1e-4
+    assert rel_err(dw, wr.grad) < 1e-4 and rel_err(db, br.grad) < 1e-4
+
+
+# ----------------------------------------------------------------------------- attention
+def ref_attn(q, k, v, causal, scale):
+    s = (q.double() @ k.double().transpose(-1, -2)) * scale
+    if causal:
+        Tq, Tk = s.shape[-2:]
+        s = s.masked_fill(torch.ones(Tq, Tk, dtype=torch.bool).triu(1 + Tk - Tq), float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    return torch.softmax(s, -1) @ v.double(), lse
+
+
+@pytest.mark.parametrize("B,H,Tq,Tk,causal", [(2, 3, 200, 200, True), (1, 2, 447, 1500, False),
+                                               (2, 2, 150, 150, False), (1, 1, 447, 447, True), (1, 2, 5, 70, False)])
+def test_attention_fwd_bwd(B, H, Tq, Tk, causal):
+    from tw import ops
+    g = torch.Generator().manual_seed(Tq + Tk)
+    d = H * 64
+    qkv_q = bf(torch.randn(B * Tq, 3 * d, generator=g))
+    kv = bf(torch.randn(B * Tk, 2 * d, generator=g))
+    q = qkv_q[:, :d]; k = kv[:, :d]; v = kv[:, d:]
+    qd, kvd = qkv_q.to(DEV), kv.to(DEV)
+    o = torch.empty(B * Tq, d, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * Tq, device=DEV)
+    scale = 0.125
+    ops.attn_fwd(qd, 3 * d, kvd, 2 * d, kvd[:, d:], 2 * d, o, d, lse, B, H, Tq, Tk, causal, scale)
+    sh = lambda t, T: t.float().view(B, T, H, 64).transpose(1, 2)
+    ref, ref_lse = ref_attn(sh(q, Tq), sh(k, Tk), sh(v, Tk), causal, scale)
+    ref = ref.transpose(1, 2).reshape(B * Tq, d)
+    assert (o.float().cpu() - ref).abs().max() < 2e-2 * ref.abs().max()
+    assert (lse.cpu().view(B, H, Tq) - ref_lse).abs().max() < 1e-3
+    # backward vs fp64 autograd on the same bf16 inputs
+    qq, kk, vv = (sh(t, T).double().requires_grad_(True) for t, T in ((q, Tq), (k, Tk), (v, Tk)))
+    s = (qq @ kk.transpose(-1, -2)) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(Tq, Tk, dtype=torch.bool).triu(1 + Tk - Tq), float("-inf"))
+    out = torch.softmax(s, -1) @ vv
+    do = bf(torch.randn(B, H, Tq, 64, generator=g))
+    out.backward(do.double())
+    dod = do.transpose(1, 2).reshape(B * Tq, d).contiguous().to(DEV)
+    dq = torch.empty(B * Tq, d, dtype=torch.bfloat16, device=DEV)
+    dkv = torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=DEV)
+    ops.attn_bwd(qd, 3 * d, kvd, 2 * d, kvd[:, d:], 2 * d, o, d, dod, d, lse, dq, d, dkv, 2 * d, dkv[:, d:], 2 * d,
+                 B, H, Tq, Tk, causal, scale)
+    torch.cuda.synchronize()
+    back = lambda t, T: t.transpose(1, 2).reshape(B * T, d)
+    for got, want, nm in ((dq, back(qq.grad, Tq), "dq"), (dkv[:, :d], back(kk.grad, Tk), "dk"),
+                          (dkv[:, d:], back(vv.grad, Tk), "dv")):
+        e = (got.float().cpu().double() - want).abs().max() / want.abs().max()
+        assert e < 3e-2, (nm, float(e))
+
+
+# ----------------------------------------------------------------------------- KL + CE
+def test_kl_ce_matches_oracle():
+    from oracle import distill_ref
+    from tw import ops
+    g = torch.Generator().manual_seed(3)
+    rows, V, ld = 37, 51865, 51904
+    s = bf(torch.randn(rows, V, generator=g) * 3).float()
+    t = bf(torch.randn(rows, V, generator=g) * 3).float()
+    labels = torch.randint(0, V, (rows,), generator=g)
+    labels[::5] = -100
+    sl = s.clone().requires_grad_(True)
+    ce = torch.nn.functional.cross_entropy(sl, labels, ignore_index=-100)
+    loss, kl = distill_ref.distill_loss(sl.unsqueeze(0), t.unsqueeze(0), labels.unsqueeze(0), ce)
+    loss.backward()
+    sd = torch.zeros(rows, ld, dtype=torch.bfloat16, device=DEV); sd[:, :V] = bf(s).to(DEV)
+    td = torch.zeros(rows, ld, dtype=torch.bfloat16, device=DEV); td[:, :V] = bf(t).to(DEV)
+    lab = labels.to(DEV)
+    nv = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.count_valid(lab, nv)
+    dl = torch.full((rows, ld), 7.0, dtype=torch.bfloat16, device=DEV)
+    out3, _ = ops.kl_ce(sd, td, lab, V, nv, dlogits=dl)
+    o = out3.cpu()
+    assert int(nv.item()) == int((labels >= 0).sum())
+    assert abs(o[1] - ce.item()) / ce.item() < 1e-4
+    assert abs(o[2] - kl.item()) / kl.item() < 1e-4
+    assert abs(o[0] - loss.item()) / loss.item() < 1e-4
+    gd = dl.float().cpu()
+    assert (gd[:, V:] == 0).all()
+    assert (gd[::5] == 0).all()
+    assert (gd[:, :V] - sl.grad).abs().max() <= 2 ** -7 * sl.grad.abs().max()
+
+
+# ----------------------------------------------------------------------------- log-mel
+def test_logmel_matches_oracle():
+    from oracle import logmel as ol
+    from tw.feature_extraction import mel_tables
+    from tw import ops
+    clips = [ol.synthetic_clip(0), ol.synthetic_clip(3, 12.0), np.zeros(16000, np.float32)]
+    wav = torch.stack([torch.from_numpy(ol.pad_or_trim(c).astype(np.float32)) for c in clips]).to(DEV)
+    basis, start, w = (t.to(DEV) for t in mel_tables())
+    mel = torch.empty(3, 80, 3000, device=DEV)
+    conv = torch.full((3, 3002, 80), 9.0, dtype=torch.bfloat16, device=DEV)
+    ops.logmel(wav, basis, start, w, mel, conv)
+    ref = ol.log_mel_batch(clips)
+    # oracle float64 vs fp32 DFT: 2e-3 abs on O(1) values
+    assert np.abs(mel.cpu().numpy() - ref).max() < 2e-3
+    c = conv.float().cpu()
+    assert (c[:, 0] == 0).all() and (c[:, 3001] == 0).all()
+    assert (c[:, 1:3001].transpose(1, 2) - bf(mel.cpu()).float()).abs().max() == 0
+
+
+# ----------------------------------------------------------------------------- misc
+def test_embed_adamw_norm_shift():
+    from tw import ops
+    g = torch.Generator().manual_seed(4)
+    V, D, B, T = 1000, 128, 3, 17
+    E, P = torch.randn(V, D, generator=g), torch.randn(448, D, generator=g)
+    ids = torch.randint(0, V, (B, T), generator=g)
+    out = torch.empty(B * T, D, device=DEV)
+    ops.embed_fwd(ids.to(DEV), E.to(DEV), P.to(DEV), out, T)
+    ref = E[ids.view(-1)] + P[torch.arange(B * T) % T]
+    assert (out.cpu() - ref).abs().max() < 1e-6
+    dh = torch.randn(B * T, D, generator=g)
+    dE = torch.zeros(V, D, device=DEV)
+    ops.embed_bwd(ids.to(DEV), dh.to(DEV), dE)
+    refE = torch.zeros(V, D).index_add_(0, ids.view(-1), dh)
+    assert (dE.cpu() - refE).abs().max() < 1e-5
+    # clip + AdamW vs torch
+    n = 10007
+    p0, gr = torch.randn(n, generator=g), torch.randn(n, generator=g) * 3
+    pt = p0.clone().requires_grad_(True); pt.grad = gr.clone()
+    gn = torch.nn.utils.clip_grad_norm_([pt], 1.0)
+    opt = torch.optim.AdamW([pt], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, foreach=False)
+    opt.step()
+    pd, gd = p0.to(DEV), gr.to(DEV)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    norm, ws = torch.zeros(1, device=DEV), torch.zeros(1024, device=DEV)
+    pb = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ops.l2norm(gd, norm, ws)
+    ops.adamw(pd, gd, m, v, pb, 1e-3, 0.9, 0.999, 1e-8, 0.01, 1, norm, 1.0)
+    assert abs(norm.item() - gn.item()) / gn.item() < 1e-5
+    assert (pd.cpu() - pt.detach()).abs().max() < 1e-6
+    assert (pb.float().cpu() - bf(pt.detach()).float()).abs().max() == 0
+    lab = torch.tensor([[5, 6, -100, -100], [50360, 1, 2, 3]])
+    out = torch.empty_like(lab, device=DEV)
+    ops.shift_tokens_right(lab.to(DEV), out, 50257, 50258)
+    assert out.cpu().tolist() == [[50258, 5, 6, 50257], [50258, 50360, 1, 2]]
