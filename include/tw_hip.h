@@ -98,6 +98,8 @@ int tw_clip_scale(float* x, int64_t n, const float* norm, float max_norm, tw_str
 int tw_im2col3(const void* src, int64_t src_rows, void* dst, int B, int T_out, int stride, int C,
                tw_stream_t stream);
 int tw_col2im_s2(const float* dA, float* dX, int B, int T_in, int T_out, int C, tw_stream_t stream);
+/* GELU backward on a bf16 activation: out = bf16(bf16(g) * gelu'(pre)). */
+int tw_gelu_bwd(const void* g, int g_dtype, const void* pre, void* out, int64_t n, tw_stream_t stream);
 
 /* teacher decoder input = shift_tokens_right(labels) (run_distillation.py:1534, HF modeling_whisper.py:68-81);
  * number of labels >= 0 (kl_divergence normaliser, run_distillation.py:1512-1515). */

@@ -45,7 +45,7 @@ def _base(d, el, dl, h, ffn, vocab=51865, max_src=1500, max_tgt=448):
 
 CONFIGS = {
     # micro: parity-test config (full vocab, real mel/encoder lengths)
-    "micro": _base(64, 2, 2, 4, 256),
+    "micro": _base(128, 2, 2, 2, 256),
     "tiny": _base(384, 4, 4, 6, 1536),
     "base": _base(512, 6, 6, 8, 2048),
     "small": _base(768, 12, 12, 12, 3072),

@@ -182,6 +182,15 @@ __global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, bf16* __
   xt[i] = f2bf(v);
 }
 
+// out = bf16( round?(g) * gelu'(pre) )  — GELU backward on an autocast bf16 activation
+__global__ void gelu_bwd_kernel(const void* __restrict__ g, int g_dtype, const bf16* __restrict__ pre,
+                                bf16* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gv = rbf(ld_as_f32(g, g_dtype, i));
+    out[i] = f2bf(gv * gelu_erf_grad(bf2f(pre[i])));
+  }
+}
+
 inline int nblocks(int64_t n, int bs, int cap = 4096) {
   int64_t b = (n + bs - 1) / bs;
   if (b > cap) b = cap;
@@ -290,6 +299,14 @@ extern "C" int tw_mel_to_conv_input(const float* mel, void* xt, int B, int nmel,
   if (n <= 0) return TW_OK;
   hipLaunchKernelGGL(mel_to_conv_input_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, mel, (bf16*)xt, B, nmel,
                      T);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_gelu_bwd(const void* g, int g_dtype, const void* pre, void* out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, g, g_dtype, (const bf16*)pre,
+                     (bf16*)out, n);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

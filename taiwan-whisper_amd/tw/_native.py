@@ -35,6 +35,7 @@ SIGNATURES = {
     "tw_clip_scale": [P, I64, P, F32, P],
     "tw_im2col3": [P, I64, P, I32, I32, I32, I32, P],
     "tw_col2im_s2": [P, P, I32, I32, I32, I32, P],
+    "tw_gelu_bwd": [P, I32, P, P, I64, P],
     "tw_shift_tokens_right": [P, P, I32, I32, I64, I64, P],
     "tw_count_valid": [P, I64, P, P],
 }

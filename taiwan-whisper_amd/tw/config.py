@@ -1,0 +1,59 @@
+"""WhisperConfig: the HF `config.json` fields the reference reads
+(`training/run_distillation.py:984-1030`, `training/create_student_model.py:131-137`).
+Unknown keys are preserved so a round-trip through save_pretrained keeps the file intact."""
+from __future__ import annotations
+
+import copy
+import json
+import os
+
+DEFAULTS = dict(
+    vocab_size=51865, num_mel_bins=80, encoder_layers=4, encoder_attention_heads=6, decoder_layers=4,
+    decoder_attention_heads=6, decoder_ffn_dim=1536, encoder_ffn_dim=1536, d_model=384,
+    max_source_positions=1500, max_target_positions=448, pad_token_id=50257, bos_token_id=50257,
+    eos_token_id=50257, decoder_start_token_id=50258, activation_function="gelu", scale_embedding=False,
+    dropout=0.0, attention_dropout=0.0, activation_dropout=0.0, layerdrop=0.0, encoder_layerdrop=0.0,
+    decoder_layerdrop=0.0, tie_word_embeddings=True, model_type="whisper",
+)
+
+
+class WhisperConfig:
+    def __init__(self, **kw):
+        d = dict(DEFAULTS)
+        d.update(kw)
+        self.__dict__.update(d)
+        if self.activation_function not in ("gelu",):
+            raise NotImplementedError(f"activation {self.activation_function}")
+        if self.d_model % self.encoder_attention_heads or self.d_model // self.encoder_attention_heads != 64:
+            raise NotImplementedError("tw kernels are specialised for head_dim 64 (every Whisper size)")
+        if self.scale_embedding:
+            raise NotImplementedError("scale_embedding=True is not used by any Whisper checkpoint")
+
+    @property
+    def head_dim(self):
+        return self.d_model // self.encoder_attention_heads
+
+    def to_dict(self):
+        return copy.deepcopy({k: v for k, v in self.__dict__.items() if not k.startswith("_")})
+
+    def update(self, d: dict):
+        self.__dict__.update(d)
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls(**d)
+
+    @classmethod
+    def from_pretrained(cls, path):
+        with open(os.path.join(path, "config.json")) as f:
+            return cls(**json.load(f))
+
+    def save_pretrained(self, path):
+        os.makedirs(path, exist_ok=True)
+        d = self.to_dict()
+        d.setdefault("architectures", ["WhisperForConditionalGeneration"])
+        with open(os.path.join(path, "config.json"), "w") as f:
+            json.dump(d, f, indent=2, sort_keys=True)
+
+    def __repr__(self):
+        return f"WhisperConfig(d_model={self.d_model}, enc={self.encoder_layers}, dec={self.decoder_layers})"

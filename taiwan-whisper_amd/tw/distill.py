@@ -1,0 +1,210 @@
+"""The distillation step — MI355X-native counterpart of the closures in
+`training/run_distillation.py`:
+
+  kl_divergence / train_step / eval_step   :1507-1578
+  freezing + share_hidden_states           :1043-1075
+  optimizer groups / AdamW / scheduler     :1425-1463 (weight decay on non-LN, non-bias names)
+  accumulate / backward / clip / step      :1662-1670 (Accelerate: loss / accum, DDP mean over ranks)
+
+Everything runs on the GPU through libtw_hip.so; nothing on the step synchronises with the host
+(metrics stay device tensors until the caller reads them).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import ops as F
+from .modeling import Backward, WhisperForConditionalGeneration, is_pseudo
+
+
+def constant_with_warmup(step: int, warmup: int) -> float:
+    """HF get_constant_schedule_with_warmup as Accelerate drives it (warmup*N, stepped N times per
+    update): update k uses lr * min(1, k / warmup)."""
+    if warmup > 0 and step < warmup:
+        return step / warmup
+    return 1.0
+
+
+def linear_schedule(step: int, warmup: int, total: int) -> float:
+    if warmup > 0 and step < warmup:
+        return step / warmup
+    return max(0.0, (total - step) / max(1, total - warmup))
+
+
+class DistillationTrainer:
+    def __init__(self, student: WhisperForConditionalGeneration, teacher: WhisperForConditionalGeneration, *,
+                 temperature: float = 2.0, kl_weight: float = 1.0, learning_rate: float = 1e-4,
+                 adam_beta1: float = 0.9, adam_beta2: float = 0.999, adam_epsilon: float = 1e-8,
+                 weight_decay: float = 0.0, max_grad_norm: float = 1.0, warmup_steps: int = 0,
+                 lr_scheduler_type: str = "constant_with_warmup", max_steps: int = 0,
+                 gradient_accumulation_steps: int = 1, freeze_encoder: bool = True, freeze_decoder: bool = False,
+                 freeze_embed_positions: bool = True, process_group=None, dp_bucket_mb: int = 64):
+        self.s, self.t = student, teacher
+        self.temperature, self.kl_weight = temperature, kl_weight
+        self.lr, self.b1, self.b2, self.eps = learning_rate, adam_beta1, adam_beta2, adam_epsilon
+        self.wd, self.max_grad_norm = weight_decay, max_grad_norm
+        self.warmup, self.sched, self.max_steps = warmup_steps, lr_scheduler_type, max_steps
+        self.accum = gradient_accumulation_steps
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.bucket = dp_bucket_mb * (1 << 20) // 4
+        # trainable set (run_distillation.py:1043-1066; HF keeps encoder.embed_positions frozen)
+        student.set_trainable("", True)
+        student.set_trainable("model.encoder.embed_positions", False)
+        if freeze_encoder:
+            student.set_trainable("model.encoder", False)
+        if freeze_decoder:
+            student.set_trainable("model.decoder", False)
+            student.set_trainable("model.decoder.embed_tokens", True)   # proj_out stays trainable
+        if freeze_embed_positions:
+            student.set_trainable("model.decoder.embed_positions", False)
+        self.train_encoder = not freeze_encoder
+        self.share = freeze_encoder and student.config.d_model == teacher.config.d_model
+        student.pack_for_training()
+        student.sync_bf16()
+        student.train()
+        teacher.eval()
+        n = student.train_prefix
+        self.m_buf = torch.zeros(n, dtype=torch.float32, device=student.device)
+        self.v_buf = torch.zeros(n, dtype=torch.float32, device=student.device)
+        self.norm = torch.zeros(1, dtype=torch.float32, device=student.device)
+        self.ws = torch.zeros(1024, dtype=torch.float32, device=student.device)
+        self.nvalid = torch.zeros(1, dtype=torch.int32, device=student.device)
+        self.step = 0            # completed optimizer updates
+        self.micro = 0
+        self.bw = Backward(student)
+        self.runs = self._wd_runs()
+
+    def _wd_runs(self):
+        """maximal [lo, hi) ranges of the trainable prefix sharing one weight decay
+        (decay group = non-LayerNorm, non-bias names, run_distillation.py:1434-1449)."""
+        s = self.s
+        runs = []
+        for n in s.train_names:
+            wd = 0.0 if ("layer_norm" in n or "bias" in n) else self.wd
+            lo = s.store.offset[n]
+            hi = lo + s.store.numel(n)
+            hi = (hi + 63) // 64 * 64
+            if runs and runs[-1][2] == wd and runs[-1][1] == lo:
+                runs[-1][1] = hi
+            else:
+                runs.append([lo, hi, wd])
+        return [tuple(r) for r in runs]
+
+    def num_trainable_parameters(self):
+        return self.s.num_parameters(only_trainable=True)
+
+    def lr_at(self, step):
+        if self.sched == "linear":
+            return self.lr * linear_schedule(step, self.warmup, self.max_steps)
+        if self.sched == "constant":
+            return self.lr
+        return self.lr * constant_with_warmup(step, self.warmup)
+
+    # ------------------------------------------------------------------ forward pieces
+    def _conv_input(self, batch):
+        if batch.get("conv_input") is not None:
+            return batch["conv_input"]
+        return self.s.conv_input(batch["input_features"])
+
+    def _teacher_logits(self, conv_in, ids, labels, enc16, Tk):
+        t = self.t
+        if self.share:
+            t_ids = torch.empty_like(labels)
+            F.shift_tokens_right(labels, t_ids, t.config.pad_token_id, t.config.decoder_start_token_id)
+            ht = t.decode(t_ids, enc16, Tk)
+        else:
+            enc_t = t.encode(conv_in)
+            ht = t.decode(ids, enc_t, Tk)
+        return t.lm_head(ht)
+
+    def train_step(self, batch, temperature: Optional[float] = None):
+        """One micro-step: student fwd + teacher fwd + fused KL/CE + backward (+ DP exchange,
+        clip and AdamW on the sync micro-step).  Returns device scalars."""
+        T = self.temperature if temperature is None else temperature
+        s = self.s
+        conv_in = self._conv_input(batch)
+        ids = batch["decoder_input_ids"].to(s.device).contiguous()
+        labels = batch["labels"].to(s.device).contiguous()
+        B, Td = ids.shape
+        if self.micro == 0:
+            s.grad.zero_()
+        enc_tape = [] if self.train_encoder else None
+        enc16 = s.encode(conv_in, tape=enc_tape)
+        Tk = enc16.shape[0] // B
+        tape = []
+        hs = s.decode(ids, enc16, Tk, tape=tape)
+        ls = s.lm_head(hs)
+        with torch.no_grad():
+            lt = self._teacher_logits(conv_in, ids, labels, enc16, Tk)
+        lab = labels.reshape(-1)
+        F.count_valid(lab, self.nvalid)
+        dlogits = torch.empty_like(ls)
+        out3, _ = F.kl_ce(ls, lt, lab, s.config.vocab_size, self.nvalid, T=T, ce_w=0.8, kl_w=self.kl_weight,
+                          grad_scale=1.0 / (self.accum * self.world), dlogits=dlogits)
+        del lt
+        d_enc = torch.zeros(B * Tk, s.config.d_model, dtype=torch.float32, device=s.device) \
+            if self.train_encoder else None
+        self.bw.decoder(tape, dlogits, hs, enc16, d_enc)
+        del tape, dlogits, ls
+        if self.train_encoder:
+            self.bw.encoder(enc_tape, d_enc)
+        self.micro += 1
+        if self.micro == self.accum:
+            self.optimizer_step()
+            self.micro = 0
+        return {"loss": out3[0], "ce_loss": out3[1], "kl_loss": out3[2]}
+
+    def eval_step(self, batch):
+        """run_distillation.py:1554-1578: T = 1, no grad."""
+        s = self.s
+        conv_in = self._conv_input(batch)
+        ids = batch["decoder_input_ids"].to(s.device).contiguous()
+        labels = batch["labels"].to(s.device).contiguous()
+        B = ids.shape[0]
+        enc16 = s.encode(conv_in)
+        Tk = enc16.shape[0] // B
+        ls = s.lm_head(s.decode(ids, enc16, Tk))
+        lt = self._teacher_logits(conv_in, ids, labels, enc16, Tk)
+        lab = labels.reshape(-1)
+        nv = torch.zeros(1, dtype=torch.int32, device=s.device)
+        F.count_valid(lab, nv)
+        out3, _ = F.kl_ce(ls, lt, lab, s.config.vocab_size, nv, T=1.0, ce_w=0.8, kl_w=self.kl_weight)
+        return {"loss": out3[0], "ce_loss": out3[1], "kl_loss": out3[2]}
+
+    # ------------------------------------------------------------------ update
+    def all_reduce_grads(self):
+        """DDP mean over ranks (the 1/world factor is already folded into the loss gradient):
+        bucketed SUM all-reduce of the flat fp32 gradient over RCCL."""
+        if self.world == 1:
+            return
+        g = self.s.grad
+        works = []
+        for lo in range(0, g.numel(), self.bucket):
+            works.append(torch.distributed.all_reduce(g[lo: lo + self.bucket], group=self.pg, async_op=True))
+        for w in works:
+            w.wait()
+
+    def optimizer_step(self):
+        s = self.s
+        self.all_reduce_grads()
+        g = s.grad
+        F.l2norm(g, self.norm, self.ws)
+        lr = self.lr_at(self.step)
+        for lo, hi, wd in self.runs:
+            F.adamw(s.store.p32[lo:hi], g[lo:hi], self.m_buf[lo:hi], self.v_buf[lo:hi], s.store.p16[lo:hi], lr,
+                    self.b1, self.b2, self.eps, wd, self.step + 1, self.norm, self.max_grad_norm)
+        self.step += 1
+        return self.norm
+
+    # ------------------------------------------------------------------ checkpoint state
+    def state_dict(self):
+        return {"step": self.step, "exp_avg": self.m_buf, "exp_avg_sq": self.v_buf}
+
+    def load_state_dict(self, st):
+        self.step = int(st["step"])
+        self.m_buf.copy_(st["exp_avg"])
+        self.v_buf.copy_(st["exp_avg_sq"])

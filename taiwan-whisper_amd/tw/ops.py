@@ -225,3 +225,9 @@ def count_valid(labels, out):
     assert labels.dtype == torch.int64 and out.dtype == torch.int32
     call("tw_count_valid", labels.data_ptr(), labels.numel(), out.data_ptr(), _stream())
     return out
+
+
+def gelu_bwd(g, pre, out):
+    assert pre.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and g.numel() == pre.numel() == out.numel()
+    call("tw_gelu_bwd", g.data_ptr(), _dt(g), pre.data_ptr(), out.data_ptr(), g.numel(), _stream())
+    return out
