@@ -1,0 +1,257 @@
+#!/usr/bin/env python
+"""Distillation-step throughput on MI355X (BASELINE.json metric: distillation utt/s on 30 s
+clips at 1/2/4/8 GPUs; teacher-fwd ms/clip).
+
+Workload (default, BASELINE config 3): 2-decoder-layer distil-whisper student made by the
+create_student_model layer map from a large-v2 teacher, frozen shared encoder, batch 64 clips per
+GPU, bf16 autocast semantics, full step = GPU log-mel + student fwd + teacher fwd + fused KL/CE +
+student bwd + (DP all-reduce) + clip + AdamW.  `--config c2` runs config 2 (whisper-small student,
+trainable encoder, full large-v2 teacher forward, B = 32).  Random-init weights of the real
+architectures (no checkpoints offline) and synthetic 30 s / 16 kHz sine clips + synthetic labels
+(SURVEY.md §8(d)); inputs are resident in HBM before the timed region.
+
+One process per GPU (torch.distributed.run); each rank processes its own 64 clips (weak scaling),
+gradients are averaged with an RCCL all-reduce; rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "taiwan-whisper_amd"))
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBS = 8000.0
+
+
+def _flops_per_clip(cfg_s, cfg_t, share, T_dec=447, T_enc=1500):
+    """Algorithmic FLOPs of one distillation step per clip (SURVEY.md §8(d) formula:
+    2*MAC of every GEMM + QK^T/PV at full size; no recompute)."""
+    def fwd(c, enc=True):
+        d, V, fe, fd = c.d_model, c.vocab_size, c.encoder_ffn_dim, c.decoder_ffn_dim
+        conv = 2 * (2 * T_enc) * (c.num_mel_bins * 3) * d + 2 * T_enc * (3 * d) * d
+        el = 2 * T_enc * d * 4 * d + 2 * 2 * T_enc * d * fe + 2 * 2 * T_enc * T_enc * d
+        dl = (2 * T_dec * d * 4 * d + 2 * 2 * T_dec * T_dec * d + 2 * T_dec * d * 2 * d + 2 * T_enc * d * 2 * d
+              + 2 * 2 * T_dec * T_enc * d + 2 * 2 * T_dec * d * fd)
+        e = conv + c.encoder_layers * el
+        return (e if enc else 0), c.decoder_layers * dl + 2 * T_dec * d * V
+    se, sd = fwd(cfg_s)
+    te, td = fwd(cfg_t)
+    if share:     # frozen shared encoder: fwd once; student decoder fwd+bwd = 3x; teacher decoder fwd
+        return se + 3 * sd + td
+    return 3 * (se + sd) + te + td
+
+
+def make_models(args, device):
+    from tw.config import WhisperConfig
+    from tw.modeling import WhisperForConditionalGeneration, random_init_
+    from tw.student import student_from_teacher
+    large = dict(d_model=1280, encoder_layers=32, decoder_layers=32, encoder_attention_heads=20,
+                 decoder_attention_heads=20, encoder_ffn_dim=5120, decoder_ffn_dim=5120)
+    small = dict(d_model=768, encoder_layers=12, decoder_layers=12, encoder_attention_heads=12,
+                 decoder_attention_heads=12, encoder_ffn_dim=3072, decoder_ffn_dim=3072)
+    tcfg = WhisperConfig(**large)
+    if args.config == "c3":
+        t32 = random_init_(WhisperForConditionalGeneration(tcfg, dtype=torch.float32, device=device), seed=0)
+        student, _, _ = student_from_teacher(t32, encoder_layers=32, decoder_layers=2)
+        teacher = WhisperForConditionalGeneration(tcfg, dtype=torch.bfloat16, device=device)
+        teacher.store.p16.copy_(t32.store.p16)   # torch_dtype=bf16 teacher (run_distillation.py:1011-1018)
+        teacher._refresh_ln32()
+        del t32
+        freeze_encoder = True
+    else:
+        teacher = random_init_(WhisperForConditionalGeneration(tcfg, dtype=torch.bfloat16, device=device), seed=0)
+        student = random_init_(WhisperForConditionalGeneration(WhisperConfig(**small), dtype=torch.float32,
+                                                               device=device), seed=1)
+        freeze_encoder = False
+    torch.cuda.empty_cache()
+    return student, teacher, freeze_encoder
+
+
+def make_batches(args, device, rank, nb=2):
+    from tw.data import DataCollatorSpeechSeq2SeqWithPadding, synthetic_audio, synthetic_label_lists
+    coll = DataCollatorSpeechSeq2SeqWithPadding(max_target_length=448)
+    out = []
+    for i in range(nb):
+        seed = 1000 * rank + i
+        wav = synthetic_audio(args.batch, seed=seed, device=device)
+        dec, lab = coll.collate_labels(synthetic_label_lists(args.batch, seed=seed))
+        out.append((wav, dec.to(device), lab.to(device)))
+    return out
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """Oracle (CPU restatement of the reference train_step, fp32, AdamW) on config 1:
+    whisper-tiny student + tiny teacher, B = 2 synthetic 30 s clips, host cores."""
+    sys.path.insert(0, REPO)
+    import numpy as np
+    from oracle import distill_ref, labels as L, logmel
+    from oracle.weights import CONFIGS, make_weights
+    from oracle.whisper_ref import Ref, to_torch
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = CONFIGS["tiny"]
+    ps = to_torch(make_weights(cfg, 1))
+    pt = to_torch(make_weights(cfg, 2))
+    names = [n for n in ps if not n.startswith("model.encoder") and "embed_positions" not in n]
+    for n in names:
+        ps[n].requires_grad_(True)
+    S, T = Ref(cfg, ps), Ref(cfg, pt)
+    B = 2
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(i) for i in range(B)]))
+    dec, lab = L.collate(L.synthetic_label_lists(B, seed=0))
+    dec, lab = torch.from_numpy(dec), torch.from_numpy(lab)
+    opt = None
+    times = []
+    t_start = time.time()
+    while True:
+        t0 = time.time()
+        # feature extraction is part of the reference step (dataloader workers, :1217)
+        feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(i) for i in range(B)]))
+        for n in names:
+            ps[n].grad = None
+        distill_ref.train_step(S, T, feats, dec, lab, share_hidden_states=True)
+        _, opt = distill_ref.optimizer_step(ps, names, lr=1e-4, state=opt)
+        times.append(time.time() - t0)
+        if time.time() - t_start > seconds_budget or len(times) >= 12:
+            break
+    steady = times[1:] if len(times) > 1 else times
+    per = sum(steady) / len(steady)
+    return dict(value=round(B / per, 4), unit="utt/s", cores=threads, kind="port",
+                sample=f"config 1 (tiny<-tiny, B=2, fp32, frozen shared encoder, CPU log-mel + train_step + "
+                       f"AdamW) via oracle/distill_ref.py, {len(steady)} steady steps of {len(times)}")
+
+
+def load_pmc(kernel_family):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary."""
+    p = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get(kernel_family, {}).get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-teacher-fwd", action="store_true")
+    args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 64 if args.config == "c3" else 32
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=device)
+        pg = torch.distributed.group.WORLD
+
+    from tw.distill import DistillationTrainer
+    from tw.feature_extraction import WhisperFeatureExtractor
+    from tw.profiling import KernelTimer
+
+    student, teacher, freeze_encoder = make_models(args, device)
+    trainer = DistillationTrainer(student, teacher, learning_rate=1e-4, warmup_steps=0,
+                                  freeze_encoder=freeze_encoder, process_group=pg)
+    fe = WhisperFeatureExtractor(device=device)
+    batches = make_batches(args, device, rank)
+
+    def step(i):
+        wav, dec, lab = batches[i % len(batches)]
+        _, conv = fe.extract(wav)
+        return trainer.train_step({"conv_input": conv, "decoder_input_ids": dec, "labels": lab})
+
+    for i in range(args.warmup):
+        m = step(i)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    timer = KernelTimer("gemm_nn")
+    with timer:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            m = step(i)
+        torch.cuda.synchronize()
+        if pg is not None:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if pg is not None:
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    loss = float(m["loss"].item())
+    ks = timer.summary()
+
+    teacher_ms = None
+    if not args.no_teacher_fwd:
+        # teacher forward (large-v2 encoder + decoder over T_dec 447 + head) ms/clip
+        wav, dec, lab = batches[0]
+        _, conv = fe.extract(wav)
+        for rep in range(4):
+            if rep == 1:
+                torch.cuda.synchronize()
+                ta = time.perf_counter()
+            enc = teacher.encode(conv)
+            teacher.lm_head(teacher.decode(dec, enc, enc.shape[0] // args.batch))
+        torch.cuda.synchronize()
+        teacher_ms = (time.perf_counter() - ta) / 3 / args.batch * 1e3
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        value = args.steps * args.batch * world / elapsed
+        flops_clip = _flops_per_clip(student.config, teacher.config, trainer.share)
+        roof = None
+        if ks is not None:
+            achieved = ks["rate"] / 1e12
+            pmc = load_pmc("gemm_nn")
+            roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                        frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=pmc,
+                        kernel="gemm_kernel<false,false> (all forward NT GEMMs of the step)",
+                        launches_per_step=ks["launches"] // args.steps, avg_launch_ms=round(ks["avg_ms"], 4),
+                        algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4))
+        out = {
+            "metric": "distillation utterances/sec (30 s clips)",
+            "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (30 s 16 kHz sines + noise, random-init weights, SURVEY.md §8d labels)",
+            "config": {"workload": ("c3: distil-32-2 student <- whisper-large-v2 teacher, frozen shared encoder"
+                                    if args.config == "c3" else
+                                    "c2: whisper-small student <- whisper-large-v2 teacher, full teacher fwd"),
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch, "seq_len": 447,
+                       "parallelism": f"dp{world}"},
+            "teacher_fwd_ms_per_clip": None if teacher_ms is None else round(teacher_ms, 3),
+            "model_tflops_per_step_per_gpu": round(flops_clip * args.batch / 1e12, 2),
+            "step_mfma_frac": round(flops_clip * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
+            "final_loss": round(loss, 4),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

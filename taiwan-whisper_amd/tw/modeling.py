@@ -529,7 +529,7 @@ class WhisperForConditionalGeneration:
             out = torch.empty(M, self.Vp, dtype=torch.bfloat16, device=self.device)
         E = self._w16("model.decoder.embed_tokens.weight")
         F.gemm(h16, E, out, M, self.Vp, self.config.d_model, lda=h16.stride(0), ldb=self.config.d_model,
-               ldc=self.Vp, flags=F.GEMM_ROUND)
+               ldc=self.Vp, flags=F.GEMM_ROUND, algo_N=self.config.vocab_size)
         return out
 
     # ------------------------------------------------------------------ HF-style forward
@@ -765,3 +765,32 @@ class Backward:
         F.im2col3(st["conv_in"], T2 + 2, A1, B, T2, 1, nm)
         self.dW(dpre1, A1, g1w, B * T2)
         self.db(dpre1, (0, d), m.gv("model.encoder.conv1.bias"))
+
+
+def random_init_(model: WhisperForConditionalGeneration, seed: int = 0, std: float = 0.02):
+    """Random weights of the right architecture on the device (benchmarks: no checkpoints offline).
+    LayerNorm = (1, 0), encoder positions = sinusoids (what checkpoints carry), pad rows 0."""
+    cfg = model.config
+    g = torch.Generator(device=model.device).manual_seed(seed)
+    st = model.store
+    buf = st.p32 if st.p32 is not None else st.p16
+    for n in st.order:
+        v = st._view(buf, n)
+        if is_pseudo(n) or n.endswith("bias"):
+            v.zero_()
+        elif "layer_norm" in n:
+            v.fill_(1.0)
+        elif n.endswith("encoder.embed_positions.weight"):
+            L, d = v.shape
+            inc = math.log(10000.0) / (d // 2 - 1)
+            inv = torch.exp(-inc * torch.arange(d // 2, device=model.device, dtype=torch.float32))
+            tt = torch.arange(L, device=model.device, dtype=torch.float32)[:, None] * inv[None, :]
+            v.copy_(torch.cat([tt.sin(), tt.cos()], 1))
+        else:
+            v.copy_(torch.randn(v.shape, generator=g, device=model.device) * std)
+            if n.endswith("embed_tokens.weight"):
+                v[cfg.vocab_size:].zero_()
+    if st.p32 is not None:
+        F.cast_bf16(st.p32, st.p16)
+    model._refresh_ln32()
+    return model

@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from ._native import call
+from .profiling import KernelTimer
 
 F32, BF16 = 0, 1
 GEMM_BIAS, GEMM_ROUND, GEMM_GELU, GEMM_RES, GEMM_ACCUM, GEMM_AUX_OUT, GEMM_DGELU = 1, 2, 4, 8, 16, 32, 64
@@ -43,7 +44,7 @@ def _need(t: torch.Tensor, n_elems: int, what: str):
 
 
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, bias=None, res=None,
-         ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0):
+         ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0, algo_N=None):
     """C[b] = epi(alpha * A[b] @ B[b]^T); A bf16 [M][K] (a_trans: [K][M]); B bf16 [N][K] (b_trans: [K][N])."""
     if M <= 0 or N <= 0:
         return C
@@ -62,9 +63,12 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     if aux is not None:
         assert aux.dtype == torch.bfloat16
         _need(aux, (batch - 1) * sAux + (M - 1) * ldaux + N, "gemm aux")
-    call("tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
-         M, N, K, batch, sA, sB, sC, float(alpha), _ptr(bias), _ptr(res), ldr, sR,
-         _dt(res) if res is not None else F32, res_mod, _ptr(aux), ldaux, sAux, flags, _stream())
+    fam = "gemm_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
+    flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
+    KernelTimer.wrap(fam, flops, lambda: call(
+        "tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
+        M, N, K, batch, sA, sB, sC, float(alpha), _ptr(bias), _ptr(res), ldr, sR,
+        _dt(res) if res is not None else F32, res_mod, _ptr(aux), ldaux, sAux, flags, _stream()))
     return C
 
 

@@ -1,0 +1,44 @@
+"""Per-launch HIP-event timing of one kernel family inside a timed region (the roofline leg of
+bench.py).  Events are recorded on the stream the kernels are launched on (torch's current
+stream, which every tw op uses)."""
+from __future__ import annotations
+
+import torch
+
+
+class KernelTimer:
+    active = None   # the KernelTimer currently collecting, or None
+
+    def __init__(self, family: str):
+        self.family = family
+        self.records = []   # (start_event, end_event, algorithmic_flops_or_bytes)
+
+    def __enter__(self):
+        KernelTimer.active = self
+        return self
+
+    def __exit__(self, *exc):
+        KernelTimer.active = None
+
+    @staticmethod
+    def wrap(family, work, launch):
+        t = KernelTimer.active
+        if t is None or t.family != family:
+            return launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = launch()
+        e1.record()
+        t.records.append((e0, e1, work))
+        return r
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b, _ in self.records]
+        work = [w for _, _, w in self.records]
+        n = len(ms)
+        if n == 0:
+            return None
+        tot_ms, tot_w = sum(ms), sum(work)
+        return dict(launches=n, avg_ms=tot_ms / n, total_ms=tot_ms, avg_work=tot_w / n,
+                    rate=tot_w / (tot_ms * 1e-3))
