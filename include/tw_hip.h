@@ -84,9 +84,9 @@ int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D
 
 /* autocast weight cast fp32 -> bf16 (ACC:accelerator.py autocast of every Linear weight). */
 int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, tw_stream_t stream);
-/* bias gradient: out[c] (+)= [bf16](sum_r x[r][c]). */
+/* bias gradient: out[c] (+)= [bf16](sum_r x[r][c]); deterministic two-pass, workspace >= ceil(rows/256)*cols. */
 int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum, int round_bf16,
-              tw_stream_t stream);
+              float* workspace, int64_t workspace_floats, tw_stream_t stream);
 
 /* clip_grad_norm_ + AdamW (run_distillation.py:1450-1455,1666-1668). */
 int tw_l2norm(const float* x, int64_t n, float* norm_out, float* workspace /* 1024 floats */, tw_stream_t stream);

@@ -45,22 +45,54 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __rest
   for (; i < n; ++i) dst[i] = f2bf(src[i]);
 }
 
-// out[c] (+)= bf16?(sum_r x[r][c]) : bias gradient of an autocast Linear (grad computed in bf16)
-__global__ void colsum_rows_kernel(const void* __restrict__ x, int x_dtype, int64_t ldx, int rows, int cols,
-                                   float* __restrict__ out, int accum, int round_bf16) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < cols)
-    for (int r = part; r < rows; r += 4) s += ld_as_f32(x, x_dtype, (int64_t)r * ldx + c);
-  red[part][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (part == 0 && c < cols) {
-    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (round_bf16) t = rbf(t);
-    out[c] = accum ? out[c] + t : t;
+// Column sums over rows (bias gradient of an autocast Linear, computed in bf16 then added to the
+// fp32 grad).  Pass 1: block (ROWS_PER x 512 columns) -> partial[chunk][cols] with 8 columns per
+// lane (16-B bf16 / 2x16-B fp32 loads); pass 2: deterministic sum over chunks (+round, +accumulate).
+constexpr int CS_COLS = 512, CS_ROWS = 256;
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restrict__ x, int x_dtype, int64_t ldx,
+                                                             int rows, int cols, float* __restrict__ partial) {
+  __shared__ float red[4][CS_COLS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * CS_COLS + lane * 8;
+  const int r0 = blockIdx.y * CS_ROWS;
+  const int r1 = min(rows, r0 + CS_ROWS);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool vec = (c0 + 7 < cols) && ((ldx & 7) == 0);
+  for (int r = r0 + wv; r < r1; r += 4) {
+    const int64_t o = (int64_t)r * ldx + c0;
+    if (vec) {
+      if (x_dtype == TW_BF16) {
+        const bf16x8 v = *(const bf16x8*)((const bf16*)x + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+      } else {
+        const f32x4 a = *(const f32x4*)((const float*)x + o);
+        const f32x4 b = *(const f32x4*)((const float*)x + o + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += b[j]; }
+      }
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < cols) acc[j] += ld_as_f32(x, x_dtype, o + j);
+    }
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wv][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < CS_COLS; c += 256) {
+    const int gc = blockIdx.x * CS_COLS + c;
+    if (gc < cols) partial[(int64_t)blockIdx.y * cols + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ partial, int nchunk, int cols, float* __restrict__ out,
+                                    int accum, int round_bf16) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float t = 0.f;
+  for (int k = 0; k < nchunk; ++k) t += partial[(int64_t)k * cols + c];
+  if (round_bf16) t = rbf(t);
+  out[c] = accum ? out[c] + t : t;
 }
 
 // sum of squares of a fp32 vector -> partial[blockIdx.x]
@@ -223,11 +255,16 @@ extern "C" int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStrea
   return TW_OK;
 }
 
+// workspace >= ceil(rows/256) * cols floats
 extern "C" int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum,
-                         int round_bf16, hipStream_t stream) {
+                         int round_bf16, float* workspace, int64_t workspace_floats, hipStream_t stream) {
   if (rows <= 0 || cols <= 0) return TW_OK;
-  hipLaunchKernelGGL(colsum_rows_kernel, dim3((cols + 63) / 64), dim3(256), 0, stream, x, x_dtype, ldx, rows, cols,
-                     out, accum, round_bf16);
+  const int nchunk = (rows + CS_ROWS - 1) / CS_ROWS;
+  if (workspace_floats < (int64_t)nchunk * cols) return TW_EINVAL;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + CS_COLS - 1) / CS_COLS, nchunk), dim3(256), 0, stream, x,
+                     x_dtype, ldx, rows, cols, workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, stream, workspace, nchunk, cols, out,
+                     accum, round_bf16);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -185,10 +185,26 @@ def cast_bf16(src, dst):
     return dst
 
 
+_WS = {}
+
+
+def workspace(n, device, key="ws"):
+    """Grow-only per-device scratch buffer (stream-ordered reuse)."""
+    k = (key, str(device))
+    t = _WS.get(k)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
+        _WS[k] = t
+    return t
+
+
 def colsum(x, ldx, rows, cols, out, accum=True, round_bf16=True):
     _need(x, (rows - 1) * ldx + cols, "colsum x")
     assert out.dtype == torch.float32 and out.numel() >= cols
-    call("tw_colsum", x.data_ptr(), _dt(x), ldx, rows, cols, out.data_ptr(), int(accum), int(round_bf16), _stream())
+    n = (rows + 255) // 256 * cols
+    ws = workspace(n, x.device, "colsum")
+    call("tw_colsum", x.data_ptr(), _dt(x), ldx, rows, cols, out.data_ptr(), int(accum), int(round_bf16),
+         ws.data_ptr(), ws.numel(), _stream())
 
 
 def l2norm(x, out, workspace):

@@ -271,3 +271,15 @@ def test_embed_adamw_norm_shift():
     out = torch.empty_like(lab, device=DEV)
     ops.shift_tokens_right(lab.to(DEV), out, 50257, 50258)
     assert out.cpu().tolist() == [[50258, 5, 6, 50257], [50258, 50360, 1, 2]]
+
+
+@pytest.mark.parametrize("rows,cols,dt", [(96000, 1280, torch.bfloat16), (1000, 5120, torch.float32),
+                                          (257, 70, torch.bfloat16)])
+def test_colsum_bias_grad(rows, cols, dt):
+    from tw import ops
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randn(rows, cols, generator=g).to(dt)
+    out = torch.ones(cols, device=DEV)
+    ops.colsum(x.to(DEV), cols, rows, cols, out, accum=True, round_bf16=True)
+    ref = bf(x.double().sum(0).float()).float() + 1.0
+    assert (out.cpu() - ref).abs().max() <= 2 ** -7 * ref.abs().max()
