@@ -1,0 +1,117 @@
+"""Data-parallel semantics on CPU with gloo, world_size 2 (no GPU needed).
+
+1. The product's gradient exchange (`DistillationTrainer.all_reduce_grads`, bucketed async SUM of
+   the flat fp32 gradient with the 1/world factor folded into the loss gradient) equals the DDP
+   mean of per-rank gradients, for bucket sizes that split the buffer unevenly.
+2. SURVEY.md §8(e) semantics on the oracle step: 2 ranks x half batch with DDP mean == 1 process
+   accumulating the two halves with loss / 2 each (per-rank token normalisation kept).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _worker_allreduce(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "taiwan-whisper_amd"))
+    from tw.distill import DistillationTrainer
+    _init(rank, world, port)
+    n = 10_007
+    g = torch.Generator().manual_seed(rank)
+    local = torch.randn(n, generator=g)
+
+    class Stub:
+        pass
+    st = Stub()
+    st.s = Stub()
+    st.s.grad = local / world            # the trainer folds 1/world into grad_scale
+    st.world, st.pg, st.bucket = world, dist.group.WORLD, 3001
+    DistillationTrainer.all_reduce_grads(st)
+    out[rank] = st.s.grad.clone()
+    dist.destroy_process_group()
+
+
+def test_allreduce_is_ddp_mean():
+    world = 2
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_worker_allreduce, args=(world, port, out), nprocs=world, join=True)
+    n = 10_007
+    mean = sum(torch.randn(n, generator=torch.Generator().manual_seed(r)) for r in range(world)) / world
+    for r in range(world):
+        assert torch.allclose(out[r], mean, atol=1e-6)
+
+
+def _worker_oracle(rank, world, port, out):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    from oracle import distill_ref, labels as L
+    from oracle.weights import CONFIGS, make_weights
+    from oracle.whisper_ref import Ref, to_torch
+    _init(rank, world, port)
+    torch.set_num_threads(2)
+    cfg = CONFIGS["micro"]
+    ps = to_torch(make_weights(cfg, 1))
+    names = [n for n in ps if n.startswith("model.decoder.layers.1")]
+    for n in names:
+        ps[n].requires_grad_(True)
+    S, T = Ref(cfg, ps), Ref(cfg, to_torch(make_weights(cfg, 2)))
+    feats = torch.from_numpy(np.random.default_rng(0).standard_normal((4, 80, 3000)).astype(np.float32) * 0.3)
+    dec, lab = L.collate(L.synthetic_label_lists(4, seed=3))
+    dec, lab = torch.from_numpy(dec), torch.from_numpy(lab)
+    sl = slice(2 * rank, 2 * rank + 2)       # batch -> rank mapping: micro-batch k*N + r
+    distill_ref.train_step(S, T, feats[sl], dec[sl], lab[sl])
+    flat = torch.cat([ps[n].grad.flatten() for n in names])
+    dist.all_reduce(flat)
+    out[rank] = flat / world
+    dist.destroy_process_group()
+
+
+def test_dp_mean_equals_accumulation_on_oracle():
+    world = 2
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_worker_oracle, args=(world, port, out), nprocs=world, join=True)
+    # single process, two micro-batches, loss / 2 each (Accelerate gradient accumulation)
+    from oracle import distill_ref, labels as L
+    from oracle.weights import CONFIGS, make_weights
+    from oracle.whisper_ref import Ref, to_torch
+    cfg = CONFIGS["micro"]
+    ps = to_torch(make_weights(cfg, 1))
+    names = [n for n in ps if n.startswith("model.decoder.layers.1")]
+    for n in names:
+        ps[n].requires_grad_(True)
+    S, T = Ref(cfg, ps), Ref(cfg, to_torch(make_weights(cfg, 2)))
+    feats = torch.from_numpy(np.random.default_rng(0).standard_normal((4, 80, 3000)).astype(np.float32) * 0.3)
+    dec, lab = L.collate(L.synthetic_label_lists(4, seed=3))
+    dec, lab = torch.from_numpy(dec), torch.from_numpy(lab)
+    acc = None
+    for k in range(2):
+        for n in names:
+            ps[n].grad = None
+        sl = slice(2 * k, 2 * k + 2)
+        distill_ref.train_step(S, T, feats[sl], dec[sl], lab[sl])
+        g = torch.cat([ps[n].grad.flatten() for n in names]) / 2
+        acc = g if acc is None else acc + g
+    for r in range(world):
+        assert torch.allclose(out[r], acc, rtol=1e-5, atol=1e-7)
