@@ -33,6 +33,8 @@ typedef void* tw_stream_t; /* hipStream_t */
 #define TW_GEMM_ACCUM 16
 #define TW_GEMM_AUX_OUT 32
 #define TW_GEMM_DGELU 64
+#define TW_GEMM_TILE128 256   /* force the 128x128 tile (A/B benchmarking) */
+#define TW_GEMM_TILE256 512   /* force the 256x256 tile */
 
 /* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
  * Replaces every nn.Linear / Conv1d (as GEMM) / tied proj_out matmul of the step, forward and

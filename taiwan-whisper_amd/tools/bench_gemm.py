@@ -1,0 +1,52 @@
+"""Interleaved A/B timing of the GEMM tile variants on the distillation step's shapes
+(MI355X_MICROARCH/cdna_hip_programming §5.4 rule 24: variants x rounds in ONE process, random data)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch
+
+from tw import ops
+
+SHAPES = [  # (name, M, N, K, a_trans, b_trans)
+    ("enc qkv", 96000, 3840, 1280, 0, 0), ("enc out", 96000, 1280, 1280, 0, 0),
+    ("enc fc1", 96000, 5120, 1280, 0, 0), ("enc fc2", 96000, 1280, 5120, 0, 0),
+    ("xattn kv", 96000, 2560, 1280, 0, 0), ("dec fc1", 28608, 5120, 1280, 0, 0),
+    ("dec out", 28608, 1280, 1280, 0, 0), ("lm head", 28608, 51904, 1280, 0, 0),
+    ("dW fc1", 5120, 1280, 28608, 1, 1), ("dX fc2", 28608, 5120, 1280, 0, 1),
+    ("dW head", 51904, 1280, 28608, 1, 1), ("dX head", 28608, 1280, 51904, 0, 1),
+]
+
+
+def main(rounds=5):
+    dev = "cuda"
+    res = {}
+    for name, M, N, K, at, bt in SHAPES:
+        A = (torch.randn(K, M, device=dev) if at else torch.randn(M, K, device=dev)).to(torch.bfloat16)
+        B = (torch.randn(K, N, device=dev) if bt else torch.randn(N, K, device=dev)).to(torch.bfloat16)
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        for variant, flag in (("t128", 256), ("t256", 512)):
+            for _ in range(2):
+                ops.gemm(A, B, C, M, N, K, lda=M if at else K, ldb=N if bt else K, ldc=N, a_trans=bool(at),
+                         b_trans=bool(bt), flags=ops.GEMM_ROUND | flag)
+        times = {"t128": [], "t256": []}
+        for r in range(rounds):
+            for variant, flag in (("t128", 256), ("t256", 512)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    ops.gemm(A, B, C, M, N, K, lda=M if at else K, ldb=N if bt else K, ldc=N, a_trans=bool(at),
+                             b_trans=bool(bt), flags=ops.GEMM_ROUND | flag)
+                e1.record()
+                torch.cuda.synchronize()
+                times[variant].append(e0.elapsed_time(e1) / 3)
+        fl = 2.0 * M * N * K
+        line = f"{name:10s} M={M:6d} N={N:6d} K={K:6d} "
+        for v in ("t128", "t256"):
+            t = sorted(times[v])[len(times[v]) // 2]
+            line += f"{v}: {t*1e3:8.1f}us {fl/t/1e9:7.1f}TF  "
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
