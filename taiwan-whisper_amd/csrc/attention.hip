@@ -85,6 +85,18 @@ struct AttnP {
 };
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+// XCD-aware bijective remap of a 2-D (blocks_per_head, heads) grid: the blocks of one
+// (batch, head) land on one XCD (blocks b and b+8 share one), so its K/V (or Q/dO) tiles are
+// fetched into that XCD's L2 once instead of once per XCD.
+__device__ __forceinline__ void remap_bh(int& xblk, int& bh) {
+  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int bid = blockIdx.y * nx + blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = bid % 8;
+  const int tid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  bh = tid / nx;
+  xblk = tid % nx;
+}
 constexpr float NEG_BIG = -1e30f;
 
 // ------------------------------------------------------------------------------------
@@ -92,8 +104,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // [2 stages][K, V]
   const int lane = lane_id(), wave = wave_id_uniform();
   const int g = lane >> 4, li = lane & 15;
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int qblk = blockIdx.x * QB;
+  int xblk, bh;
+  remap_bh(xblk, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  const int qblk = xblk * QB;
   const int qw = qblk + wave * QW;
   const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + h * 64;
   const bf16* Kb = p.K + (int64_t)b * p.Tk * p.ldk + h * 64;
@@ -132,9 +146,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
 
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
     const char* Ks = smem + cur * 2 * TB;
     const char* Vs = Ks + TB;
+    // all K and V fragments of this tile into registers BEFORE the next tile's LDS-DMA is
+    // issued: otherwise the compiler cannot prove the DMA does not alias these reads and
+    // drains vmcnt(0) in the middle of the tile (exposing the whole load latency)
+    bf16x8 kf[4][2], vf[4][2];
+#pragma unroll
+    for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) kf[kj][kk] = rd_row(Ks, kj * 16, kk, lane);
+#pragma unroll
+    for (int hj = 0; hj < 4; ++hj)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) vf[hj][ss] = rd_tr(Vs, hj * 16, ss, lane);
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
     // S^T = K Q^T
     f32x4 s[4][2];
 #pragma unroll
@@ -143,44 +169,56 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
       s[kj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8 kf = rd_row(Ks, kj * 16, kk, lane);
-        s[kj][0] = MFMA(kf, qf[0][kk], s[kj][0]);
-        s[kj][1] = MFMA(kf, qf[1][kk], s[kj][1]);
+        s[kj][0] = MFMA(kf[kj][kk], qf[0][kk], s[kj][0]);
+        s[kj][1] = MFMA(kf[kj][kk], qf[1][kk], s[kj][1]);
       }
     }
-    // online softmax (log2 domain), per query column
+    // online softmax (log2 domain), per query column.  Masking only on boundary tiles
+    // (key tail / causal diagonal); max on raw scores (scale > 0); p = exp2(s*c - m) is one
+    // FMA + one exp; O is rescaled only when some row max of this wave grew.
     const int k0 = kt * KT;
+    const bool need_mask = (k0 + KT > p.Tk) || (p.causal && k0 + KT - 1 > qw + off);
+    if (need_mask) {
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        const int q = qw + qi * 16 + li;
+#pragma unroll
+        for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + kj * 16 + 4 * g + r;
+            const bool ok = key < p.Tk && (!p.causal || key <= q + off);
+            if (!ok) s[kj][qi][r] = -INFINITY;
+          }
+      }
+    }
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
-      const int q = qw + qi * 16 + li;
-      float tmax = NEG_BIG;
+      float tmax = -INFINITY;
 #pragma unroll
       for (int kj = 0; kj < 4; ++kj)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + kj * 16 + 4 * g + r;
-          const bool ok = key < p.Tk && (!p.causal || key <= q + off);
-          const float x = ok ? s[kj][qi][r] * p.scale_log2 : -INFINITY;
-          s[kj][qi][r] = x;
-          tmax = fmaxf(tmax, x);
-        }
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[kj][qi][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m[qi], tmax);
-      const float alpha = exp2f(m[qi] - mn);
+      const float mn = fmaxf(m[qi], tmax * p.scale_log2);
+      if (__any(mn > m[qi])) {
+        const float alpha = __builtin_amdgcn_exp2f(m[qi] - mn);
+        l[qi] *= alpha;
+#pragma unroll
+        for (int hj = 0; hj < 4; ++hj) o[hj][qi] *= alpha;
+      }
       m[qi] = mn;
       float ls = 0.f;
 #pragma unroll
       for (int kj = 0; kj < 4; ++kj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(s[kj][qi][r] - mn);
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[kj][qi][r], p.scale_log2, -mn));
           s[kj][qi][r] = e;
           ls += e;
         }
-      l[qi] = l[qi] * alpha + ls;
-#pragma unroll
-      for (int hj = 0; hj < 4; ++hj) o[hj][qi] *= alpha;
+      l[qi] += ls;
     }
     // O^T += V^T P^T
 #pragma unroll
@@ -189,9 +227,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
       const bf16x8 p1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
 #pragma unroll
       for (int hj = 0; hj < 4; ++hj) {
-        const bf16x8 vf = rd_tr(Vs, hj * 16, ss, lane);
-        o[hj][0] = MFMA(vf, p0, o[hj][0]);
-        o[hj][1] = MFMA(vf, p1, o[hj][1]);
+        o[hj][0] = MFMA(vf[hj][ss], p0, o[hj][0]);
+        o[hj][1] = MFMA(vf[hj][ss], p1, o[hj][1]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -240,8 +277,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];
   const int lane = lane_id(), wave = wave_id_uniform();
   const int g = lane >> 4, li = lane & 15;
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int qblk = blockIdx.x * QB;
+  int xblk, bh;
+  remap_bh(xblk, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  const int qblk = xblk * QB;
   const int qw = qblk + wave * QW;
   const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + h * 64;
   const bf16* dOb = p.dO + (int64_t)b * p.Tq * p.lddo + h * 64;
@@ -349,8 +388,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB + 2 * 2 * 64 * 4];
   const int lane = lane_id(), wave = wave_id_uniform();
   const int g = lane >> 4, li = lane & 15;
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int kblk = blockIdx.x * QB;
+  int xblk, bh;
+  remap_bh(xblk, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  const int kblk = xblk * QB;
   const int kw = kblk + wave * QW;
   const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + h * 64;
   const bf16* dOb = p.dO + (int64_t)b * p.Tq * p.lddo + h * 64;

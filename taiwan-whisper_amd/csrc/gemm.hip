@@ -153,25 +153,47 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
     const char* As = smem + cur * (A_BYTES + B_BYTES);
     const char* Bs = As + A_BYTES;
+    if constexpr (AT || BT) {
+      // transposed (ds_read_b64_tr_b16) reads: fetch both k-halves BEFORE the next stage's
+      // LDS-DMA is issued, else the compiler cannot prove they do not alias the DMA and
+      // drains vmcnt(0) mid-step (the whole load latency exposed every K-step)
+      bf16x8 a[2][FM], b[2][FN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 a[FM], b[FN];
-#pragma unroll
-      for (int ni = 0; ni < FN; ++ni)
-        b[ni] = BT ? frag_mn<BN>(Bs, wn * (BN / WN) + ni * 16, kk, lane)
-                   : frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
-#pragma unroll
-      for (int mi = 0; mi < FM; ++mi)
-        a[mi] = AT ? frag_mn<BM>(As, wm * (BM / WM) + mi * 16, kk, lane)
-                   : frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
-#pragma unroll
-      for (int mi = 0; mi < FM; ++mi)
+      for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
         for (int ni = 0; ni < FN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
+          b[kk][ni] = BT ? frag_mn<BN>(Bs, wn * (BN / WN) + ni * 16, kk, lane)
+                         : frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+          a[kk][mi] = AT ? frag_mn<BM>(As, wm * (BM / WM) + mi * 16, kk, lane)
+                         : frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
+      }
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < FN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][ni], a[kk][mi], acc[mi][ni], 0, 0, 0);
+    } else {
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 a[FM], b[FN];
+#pragma unroll
+        for (int ni = 0; ni < FN; ++ni) b[ni] = frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi) a[mi] = frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < FN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
