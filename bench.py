@@ -154,11 +154,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TW_BENCH_REHEARSE=1: all ranks on cuda:0 over gloo (multi-rank rehearsal on a 1-GPU box);
+    # the real multi-GPU run uses one GPU per rank and RCCL ("nccl").
+    rehearse = os.environ.get("TW_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     pg = None
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=device)
+        if rehearse:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=device)
         pg = torch.distributed.group.WORLD
 
     from tw.distill import DistillationTrainer
