@@ -35,6 +35,7 @@ typedef void* tw_stream_t; /* hipStream_t */
 #define TW_GEMM_DGELU 64
 #define TW_GEMM_TILE128 256   /* force the 128x128 tile (A/B benchmarking) */
 #define TW_GEMM_TILE256 512   /* force the 256x256 tile */
+#define TW_GEMM_TILE256x128 1024  /* force the 256x128 tile with the 3-stage LDS ring */
 
 /* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
  * Replaces every nn.Linear / Conv1d (as GEMM) / tied proj_out matmul of the step, forward and

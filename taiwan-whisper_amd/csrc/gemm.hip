@@ -109,12 +109,27 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* tile, int cbase, int kk, i
 // Block tile BMxBN, waves WMxWN (each (BM/WM)x(BN/WN)), two LDS stages, one barrier per K-step.
 // blockIdx.x enumerates (m-tile, n-tile) pairs remapped so that consecutive tiles of one m-row
 // share an XCD (L2 reuse of the A panel; blocks b and b+8 share an XCD).
-template <bool AT, bool BT, int BM, int BN, int WM, int WN>
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {   // s_waitcnt vmcnt(N) lgkmcnt(0), N compile-time
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+  else static_assert(N < 0, "add the vmcnt immediate");
+}
+
+// STAGES-deep LDS ring, prefetch distance STAGES-1; waits are counted (vmcnt = loads of the
+// stages allowed to stay in flight) and the barrier is a raw s_barrier, so in-flight LDS-DMA
+// survives it (a __syncthreads() would drain vmcnt(0)).
+template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
   constexpr int NW = WM * WN;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  constexpr int PD = STAGES - 1;                          // prefetch distance (K-steps)
+  constexpr int LPS = BM / 8 / NW + BN / 8 / NW;          // LDS-DMA instructions per stage per wave
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
   const int lane = lane_id();
   const int wave = wave_id_uniform();
   const int wm = wave / WN, wn = wave % WN;
@@ -147,12 +162,15 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
     else    stage_k<BN, NW>(B + (int64_t)n0 * p.ldb + k0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
   };
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  for (int s = 0; s < PD; ++s)
+    if (s < nk) stage(s, s);
+  if (nk >= PD) wait_vm_lgkm0<(PD - 1) * LPS>();     // stage 0 landed, later ones may fly
+  else wait_vm_lgkm0<0>();
+  __builtin_amdgcn_s_barrier();
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = kt % STAGES;
+    const int nxt = (kt + PD) % STAGES;
     const char* As = smem + cur * (A_BYTES + B_BYTES);
     const char* Bs = As + A_BYTES;
     if constexpr (AT || BT) {
@@ -171,7 +189,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
           a[kk][mi] = AT ? frag_mn<BM>(As, wm * (BM / WM) + mi * 16, kk, lane)
                          : frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
       }
-      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      if (kt + PD < nk) stage(nxt, kt + PD);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -180,7 +198,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
           for (int ni = 0; ni < FN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][ni], a[kk][mi], acc[mi][ni], 0, 0, 0);
     } else {
-      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      if (kt + PD < nk) stage(nxt, kt + PD);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         bf16x8 a[FM], b[FN];
@@ -195,8 +213,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // stage kt+1 must have landed; stages kt+2 .. kt+PD (when issued) may stay in flight
+    if (kt + PD < nk) wait_vm_lgkm0<(PD - 1) * LPS>();
+    else wait_vm_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();
   }
 
   // ---- epilogue: lane holds C[m][n..n+3] per fragment
@@ -339,18 +359,19 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
   }
 }
 
-template <bool AT, bool BT, int BM, int BN, int WM, int WN>
+template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
 void launch(GemmP p, int batch, hipStream_t stream) {
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_mn = p.tiles_n * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_kernel<AT, BT, BM, BN, WM, WN>), dim3(p.tiles_mn, 1, batch), dim3(WM * WN * 64), 0, stream,
-                     p);
+  hipLaunchKernelGGL((gemm_kernel<AT, BT, BM, BN, WM, WN, STAGES>), dim3(p.tiles_mn, 1, batch), dim3(WM * WN * 64), 0,
+                     stream, p);
 }
 
 template <bool AT, bool BT>
 void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
-  if (tile == 256) launch<AT, BT, 256, 256, 2, 4>(p, batch, stream);
-  else launch<AT, BT, 128, 128, 2, 2>(p, batch, stream);
+  if (tile == 256) launch<AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
+  else if (tile == 2561) launch<AT, BT, 256, 128, 4, 2, 3>(p, batch, stream);
+  else launch<AT, BT, 128, 128, 2, 2, 2>(p, batch, stream);
 }
 
 }  // namespace
@@ -379,9 +400,15 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux; p.c_dtype = c_dtype; p.flags = flags;
   // 256x256 tiles (8 waves) when the problem has enough tiles to fill the chip, else 128x128
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
-  int tile = (t256 >= 1000 && K >= 256) ? 256 : 128;   // measured crossover (tools/bench_gemm.py)
+  const int64_t t2561 = (int64_t)((M + 255) / 256) * ((N + 127) / 128) * batch;
+  // measured crossovers (tools/bench_gemm.py, r01): the 3-stage 256x128 ring wins by 8-12% on
+  // the K<=4096 NN/NT shapes; long-K reductions (dW, dX of the vocab head) keep the 2-stage
+  // 256x256 tile, small grids the 128x128 one.
+  int tile = (t256 >= 1000 && K >= 256) ? 256 : 128;
+  if (!a_trans && K >= 256 && K <= 4096 && t2561 >= 1500) tile = 2561;
   if (flags & 256) tile = 128;        // forced tile (benchmarking / A-B comparisons)
   if (flags & 512) tile = 256;
+  if (flags & 1024) tile = 2561;      // 256x128, 3-stage ring
   const int64_t ntiles = tile == 256 ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (ntiles > 0x7fffffff || batch > 65535) return TW_EINVAL;
   if (!a_trans && !b_trans) dispatch<false, false>(p, batch, stream, tile);

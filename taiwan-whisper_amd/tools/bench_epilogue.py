@@ -23,6 +23,9 @@ def t(fn, rounds=5, reps=3):
     return sorted(out)[len(out) // 2]
 
 
+VARIANTS = (("t256", ops.GEMM_TILE256), ("s3", ops.GEMM_TILE256x128))
+
+
 def main():
     dev = "cuda"
     M, K = 96000, 1280
@@ -34,19 +37,26 @@ def main():
         Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
         Cf = torch.empty(M, N, dtype=torch.float32, device=dev)
         res = torch.randn(M, N, device=dev)
+        resb = torch.randn(M, N, device=dev).bfloat16()
         fl = 2.0 * M * N * Kk
         cases = {
-            "round bf16": lambda: ops.gemm(A, W, Cb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, flags=ops.GEMM_ROUND),
-            "bias+round": lambda: ops.gemm(A, W, Cb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b, flags=ops.GEMM_ROUND),
-            "bias+gelu": lambda: ops.gemm(A, W, Cb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b,
-                                          flags=ops.GEMM_ROUND | ops.GEMM_GELU),
-            "f32 out": lambda: ops.gemm(A, W, Cf, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, flags=0),
-            "bias+res f32 inplace": lambda: ops.gemm(A, W, res, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b, res=res,
-                                                     ldr=N, flags=ops.GEMM_ROUND),
+            "round bf16": lambda f: ops.gemm(A, W, Cb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, flags=ops.GEMM_ROUND | f),
+            "bias+round": lambda f: ops.gemm(A, W, Cb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b,
+                                             flags=ops.GEMM_ROUND | f),
+            "bias+gelu": lambda f: ops.gemm(A, W, Cb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b,
+                                            flags=ops.GEMM_ROUND | ops.GEMM_GELU | f),
+            "f32 out": lambda f: ops.gemm(A, W, Cf, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, flags=f),
+            "bias+res f32 inplace": lambda f: ops.gemm(A, W, res, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b, res=res,
+                                                       ldr=N, flags=ops.GEMM_ROUND | f),
+            "bias+res bf16 inplace": lambda f: ops.gemm(A, W, resb, M, N, Kk, lda=Kk, ldb=Kk, ldc=N, bias=b,
+                                                        res=resb, ldr=N, flags=ops.GEMM_ROUND | f),
         }
         for cname, fn in cases.items():
-            ms = t(fn)
-            print(f"{name:4s} N={N:5d} K={Kk:5d} {cname:22s} {ms*1e3:8.1f}us {fl/ms/1e9:7.1f}TF", flush=True)
+            line = f"{name:4s} N={N:5d} K={Kk:5d} {cname:22s}"
+            for vname, vf in VARIANTS:
+                ms = t(lambda: fn(vf))
+                line += f" {vname}: {ms*1e3:7.1f}us {fl/ms/1e9:6.1f}TF"
+            print(line, flush=True)
 
 
 if __name__ == "__main__":

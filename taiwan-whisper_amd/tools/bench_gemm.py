@@ -8,6 +8,7 @@ import torch
 
 from tw import ops
 
+VARIANTS = (("t128", 256), ("t256", 512), ("t256x128s3", 1024))
 SHAPES = [  # (name, M, N, K, a_trans, b_trans)
     ("enc qkv", 96000, 3840, 1280, 0, 0), ("enc out", 96000, 1280, 1280, 0, 0),
     ("enc fc1", 96000, 5120, 1280, 0, 0), ("enc fc2", 96000, 1280, 5120, 0, 0),
@@ -25,13 +26,13 @@ def main(rounds=5):
         A = (torch.randn(K, M, device=dev) if at else torch.randn(M, K, device=dev)).to(torch.bfloat16)
         B = (torch.randn(K, N, device=dev) if bt else torch.randn(N, K, device=dev)).to(torch.bfloat16)
         C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        for variant, flag in (("t128", 256), ("t256", 512)):
+        for variant, flag in VARIANTS:
             for _ in range(2):
                 ops.gemm(A, B, C, M, N, K, lda=M if at else K, ldb=N if bt else K, ldc=N, a_trans=bool(at),
                          b_trans=bool(bt), flags=ops.GEMM_ROUND | flag)
-        times = {"t128": [], "t256": []}
+        times = {v: [] for v, _ in VARIANTS}
         for r in range(rounds):
-            for variant, flag in (("t128", 256), ("t256", 512)):
+            for variant, flag in VARIANTS:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(3):
@@ -42,7 +43,7 @@ def main(rounds=5):
                 times[variant].append(e0.elapsed_time(e1) / 3)
         fl = 2.0 * M * N * K
         line = f"{name:10s} M={M:6d} N={N:6d} K={K:6d} "
-        for v in ("t128", "t256"):
+        for v, _ in VARIANTS:
             t = sorted(times[v])[len(times[v]) // 2]
             line += f"{v}: {t*1e3:8.1f}us {fl/t/1e9:7.1f}TF  "
         print(line, flush=True)
