@@ -234,7 +234,9 @@ def main():
             pmc = load_pmc("gemm_nn")
             roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=pmc,
-                        kernel="gemm_kernel<false,false> (all forward NT GEMMs of the step)",
+                        kernel="tw_gemm_bf16 K-major x K-major launches (every forward X.W^T of the step): "
+                               "gemm_pp_kernel (persistent 256x256 ping-pong) + gemm_kernel<false,false,128,...> "
+                               "for grids under ~1000 256-tiles",
                         launches_per_step=ks["launches"] // args.steps, avg_launch_ms=round(ks["avg_ms"], 4),
                         algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4))
         out = {

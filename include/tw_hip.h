@@ -36,6 +36,7 @@ typedef void* tw_stream_t; /* hipStream_t */
 #define TW_GEMM_TILE128 256   /* force the 128x128 tile (A/B benchmarking) */
 #define TW_GEMM_TILE256 512   /* force the 256x256 tile */
 #define TW_GEMM_TILE256x128 1024  /* force the 256x128 tile with the 3-stage LDS ring */
+#define TW_GEMM_TILE256PP 2048    /* force the 256x256 ping-pong kernel (a_trans = b_trans = 0 only) */
 
 /* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
  * Replaces every nn.Linear / Conv1d (as GEMM) / tied proj_out matmul of the step, forward and

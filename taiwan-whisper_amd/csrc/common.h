@@ -34,12 +34,26 @@ __device__ __forceinline__ float ld_as_f32(const void* p, int dtype, int64_t i) 
   return dtype == TW_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
 }
 
-__device__ __forceinline__ float gelu_erf(float x) {   // exact GELU (HF ACT2FN["gelu"])
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+// erf, branch-free (Abramowitz & Stegun 7.1.26: |error| <= 1.5e-7 absolute, ~14 VALU, no
+// divergent polynomial pair as in the libm erff): GELU sits in GEMM epilogues, where every VALU
+// of a 256x256 tile is exposed.
+__device__ __forceinline__ float erf_fast(float z) {
+  const float a = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float q = fmaf(1.061405429f, t, -1.453152027f);
+  q = fmaf(q, t, 1.421413741f);
+  q = fmaf(q, t, -0.284496736f);
+  q = fmaf(q, t, 0.254829592f);
+  q *= t;
+  const float e = __builtin_amdgcn_exp2f(-(a * a) * 1.44269504088896341f);
+  return copysignf(fmaf(-q, e, 1.0f), z);
+}
+__device__ __forceinline__ float gelu_erf(float x) {   // GELU (HF ACT2FN["gelu"], erf form)
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f));
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
-  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);
   return cdf + x * pdf;
 }
 

@@ -18,6 +18,8 @@
 // 4 consecutive output columns of one row: 8/16-B stores in the epilogue.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int BK = 64;
@@ -42,7 +44,8 @@ struct GemmP {
   const void* res; int64_t ldr; int64_t sR; int res_dtype; int res_mod;
   bf16* aux; int64_t ldaux; int64_t sAux;
   int c_dtype; int flags;
-  int tiles_n, tiles_mn;
+  int tiles_n, tiles_mn, group_m, tiles_total;
+  int epi;         // fast epilogue kind chosen on the host (EPI_*), EPI_GENERIC otherwise
 };
 
 __device__ __forceinline__ int xr_mn(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -119,107 +122,25 @@ __device__ __forceinline__ void wait_vm_lgkm0() {   // s_waitcnt vmcnt(N) lgkmcn
   else static_assert(N < 0, "add the vmcnt immediate");
 }
 
-// STAGES-deep LDS ring, prefetch distance STAGES-1; waits are counted (vmcnt = loads of the
-// stages allowed to stay in flight) and the barrier is a raw s_barrier, so in-flight LDS-DMA
-// survives it (a __syncthreads() would drain vmcnt(0)).
-template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
-  constexpr int NW = WM * WN;
+// Linear tile id -> (m-tile, n-tile), grouped: runs of group_m m-tiles are walked n-tile by
+// n-tile, so the ~32 tiles one XCD holds at a time share group_m A panels and 32/group_m B
+// panels in its L2 (group_m = 1: plain row-major).
+__device__ __forceinline__ void tile_coords(int tid, const GemmP& p, int& mt, int& nt) {
+  const int tiles_m = p.tiles_mn / p.tiles_n;
+  const int per_group = p.group_m * p.tiles_n;
+  const int g = tid / per_group, first = g * p.group_m;
+  const int gm = min(p.group_m, tiles_m - first);
+  const int r = tid - g * per_group;
+  mt = first + r % gm;
+  nt = r / gm;
+}
+
+// Generic epilogue (any flag combination, ragged edges): lane holds C[m][n..n+3] of each 16x16
+// fragment (swapped-operand MFMA layout).
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                         int n0, int wm, int wn, int lane, int bz) {
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int PD = STAGES - 1;                          // prefetch distance (K-steps)
-  constexpr int LPS = BM / 8 / NW + BN / 8 / NW;          // LDS-DMA instructions per stage per wave
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
-  const int lane = lane_id();
-  const int wave = wave_id_uniform();
-  const int wm = wave / WN, wn = wave % WN;
-  const int bz = blockIdx.z;
-  // XCD-aware bijective remap of the linear tile id
-  const int nwg = p.tiles_mn, bid = blockIdx.x;
-  const int q = nwg / 8, rr = nwg % 8, xcd = bid % 8;
-  const int tid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  const int mt = tid / p.tiles_n, nt = tid % p.tiles_n;
-  const int n0 = nt * BN, m0 = mt * BM;
-
-  const bf16* A = p.A + bz * p.sA;
-  const bf16* B = p.B + bz * p.sB;
-  const int K = p.K;
-  const int nk = (K + BK - 1) / BK;
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto stage = [&](int buf, int kt) {
-    char* As = smem + buf * (A_BYTES + B_BYTES);
-    char* Bs = As + A_BYTES;
-    const int k0 = kt * BK;
-    if (AT) stage_mn<BM, NW>(A + (int64_t)k0 * p.lda + m0, p.lda, p.M - m0, K - k0, As, wave, lane);
-    else    stage_k<BM, NW>(A + (int64_t)m0 * p.lda + k0, p.lda, p.M - m0, K - k0, As, wave, lane);
-    if (BT) stage_mn<BN, NW>(B + (int64_t)k0 * p.ldb + n0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
-    else    stage_k<BN, NW>(B + (int64_t)n0 * p.ldb + k0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
-  };
-
-  for (int s = 0; s < PD; ++s)
-    if (s < nk) stage(s, s);
-  if (nk >= PD) wait_vm_lgkm0<(PD - 1) * LPS>();     // stage 0 landed, later ones may fly
-  else wait_vm_lgkm0<0>();
-  __builtin_amdgcn_s_barrier();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt % STAGES;
-    const int nxt = (kt + PD) % STAGES;
-    const char* As = smem + cur * (A_BYTES + B_BYTES);
-    const char* Bs = As + A_BYTES;
-    if constexpr (AT || BT) {
-      // transposed (ds_read_b64_tr_b16) reads: fetch both k-halves BEFORE the next stage's
-      // LDS-DMA is issued, else the compiler cannot prove they do not alias the DMA and
-      // drains vmcnt(0) mid-step (the whole load latency exposed every K-step)
-      bf16x8 a[2][FM], b[2][FN];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int ni = 0; ni < FN; ++ni)
-          b[kk][ni] = BT ? frag_mn<BN>(Bs, wn * (BN / WN) + ni * 16, kk, lane)
-                         : frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
-#pragma unroll
-        for (int mi = 0; mi < FM; ++mi)
-          a[kk][mi] = AT ? frag_mn<BM>(As, wm * (BM / WM) + mi * 16, kk, lane)
-                         : frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
-      }
-      if (kt + PD < nk) stage(nxt, kt + PD);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int mi = 0; mi < FM; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < FN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][ni], a[kk][mi], acc[mi][ni], 0, 0, 0);
-    } else {
-      if (kt + PD < nk) stage(nxt, kt + PD);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 a[FM], b[FN];
-#pragma unroll
-        for (int ni = 0; ni < FN; ++ni) b[ni] = frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
-#pragma unroll
-        for (int mi = 0; mi < FM; ++mi) a[mi] = frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
-#pragma unroll
-        for (int mi = 0; mi < FM; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < FN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
-      }
-    }
-    // stage kt+1 must have landed; stages kt+2 .. kt+PD (when issued) may stay in flight
-    if (kt + PD < nk) wait_vm_lgkm0<(PD - 1) * LPS>();
-    else wait_vm_lgkm0<0>();
-    __builtin_amdgcn_s_barrier();
-  }
-
-  // ---- epilogue: lane holds C[m][n..n+3] per fragment
   const int g = lane >> 4, li = lane & 15;
   const int flags = p.flags;
   char* C = (char*)p.C;
@@ -359,6 +280,432 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Specialised full-tile epilogues for the step's hot flag combinations (chosen on the host, so
+// the per-element code carries no flag branches).  bf16 tiles are written 16 B per lane: the
+// fragments (ni, ni+1) of one row block are exchanged with v_permlane16_swap, after which lane
+// (li, g) holds 8 consecutive columns at  16*ni + (g&1)*16 + (g>>1)*8  (64 contiguous bytes per
+// row per store instruction instead of 32).  The same exchange maps a 16-B residual load back
+// to fragment order (the swap is an involution), so each lane reads and writes the same bytes
+// (in-place residual updates stay race-free).
+// ---------------------------------------------------------------------------------------------
+enum { EPI_GENERIC = 0, EPI_STORE_BF16, EPI_STORE_F32, EPI_GELU, EPI_GELU_AUX, EPI_RES_BF16, EPI_RES_F32 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  return __builtin_bit_cast(uint32_t, bf16x2{f2bf(a), f2bf(b)});
+}
+__device__ __forceinline__ float lo_bf(uint32_t u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+
+// fragments X (ni) and Y (ni+1), 4 floats each -> this lane's 16 B of the pair (swapped layout)
+__device__ __forceinline__ u32x4 pair_to_u4(const float (&x)[4], const float (&y)[4]) {
+  const uint32_t x0 = pack2(x[0], x[1]), x1 = pack2(x[2], x[3]);
+  const uint32_t y0 = pack2(y[0], y[1]), y1 = pack2(y[2], y[3]);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+  return u32x4{s0[0], s1[0], s0[1], s1[1]};
+}
+// inverse: this lane's 16 B of the pair (swapped layout) -> fragments X, Y as floats
+__device__ __forceinline__ void u4_to_pair(u32x4 r, float (&x)[4], float (&y)[4]) {
+  const auto s0 = __builtin_amdgcn_permlane16_swap(r[0], r[2], false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(r[1], r[3], false, false);
+  x[0] = lo_bf(s0[0]); x[1] = hi_bf(s0[0]); x[2] = lo_bf(s1[0]); x[3] = hi_bf(s1[0]);
+  y[0] = lo_bf(s0[1]); y[1] = hi_bf(s0[1]); y[2] = lo_bf(s1[1]); y[3] = hi_bf(s1[1]);
+}
+
+template <int BM, int BN, int WM, int WN, int KIND>
+__device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                              int n0, int wm, int wn, int lane, int bz) {
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  static_assert(FN % 2 == 0, "fragment pairs");
+  const int g = lane >> 4, li = lane & 15;
+  const int cw = n0 + wn * (BN / WN);                 // wave's first column
+  const int sw = (g & 1) * 16 + (g >> 1) * 8;        // this lane's column in a swapped pair
+  const bool rnd = p.flags & F_ROUND;
+  float bv[FN][4];
+#pragma unroll
+  for (int ni = 0; ni < FN; ++ni) {
+    if (p.flags & F_BIAS) {
+      const bf16x4 t = *(const bf16x4*)(p.bias + cw + ni * 16 + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[ni][r] = bf2f(t[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < FM; ++mi) {
+    const int64_t m = m0 + wm * (BM / WM) + mi * 16 + li;
+    // residual operand of the whole row block, loaded before any store of it
+    u32x4 rb[FN / 2];
+    f32x4 rf[FN];
+    if constexpr (KIND == EPI_RES_BF16) {
+      const bf16* rrow = (const bf16*)p.res + bz * p.sR + m * p.ldr + cw;
+#pragma unroll
+      for (int np = 0; np < FN / 2; ++np) rb[np] = *(const u32x4*)(rrow + np * 32 + sw);
+    }
+    if constexpr (KIND == EPI_RES_F32) {
+      const float* rrow = (const float*)p.res + bz * p.sR + m * p.ldr + cw;
+#pragma unroll
+      for (int ni = 0; ni < FN; ++ni) rf[ni] = *(const f32x4*)(rrow + ni * 16 + 4 * g);
+    }
+#pragma unroll
+    for (int np = 0; np < FN / 2; ++np) {
+      float v[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[h][r] = p.alpha * acc[mi][2 * np + h][r] + bv[2 * np + h][r];
+      if constexpr (KIND == EPI_STORE_BF16) {
+        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+      } else if constexpr (KIND == EPI_STORE_F32) {
+        float* crow = (float*)p.C + bz * p.sC + m * p.ldc + cw;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = rnd ? rbf(v[h][r]) : v[h][r];
+          *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
+        }
+      } else if constexpr (KIND == EPI_GELU || KIND == EPI_GELU_AUX) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[h][r] = rbf(v[h][r]);     // autocast: Linear output is bf16
+        if constexpr (KIND == EPI_GELU_AUX) {
+          bf16* arow = p.aux + bz * p.sAux + m * p.ldaux + cw;
+          *(u32x4*)(arow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[h][r] = gelu_erf(v[h][r]);
+        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+      } else if constexpr (KIND == EPI_RES_BF16) {
+        float x[4], y[4];
+        u4_to_pair(rb[np], x, y);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[0][r] = (rnd ? rbf(v[0][r]) : v[0][r]) + x[r];
+          v[1][r] = (rnd ? rbf(v[1][r]) : v[1][r]) + y[r];
+        }
+        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+      } else {   // EPI_RES_F32
+        float* crow = (float*)p.C + bz * p.sC + m * p.ldc + cw;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (rnd ? rbf(v[h][r]) : v[h][r]) + rf[2 * np + h][r];
+          *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                         int n0, int wm, int wn, int lane, int bz) {
+  const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
+  const int k = full ? p.epi : EPI_GENERIC;
+  if (k == EPI_STORE_BF16) epilogue_fast<BM, BN, WM, WN, EPI_STORE_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_STORE_F32) epilogue_fast<BM, BN, WM, WN, EPI_STORE_F32>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_GELU) epilogue_fast<BM, BN, WM, WN, EPI_GELU>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_GELU_AUX) epilogue_fast<BM, BN, WM, WN, EPI_GELU_AUX>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_RES_BF16) epilogue_fast<BM, BN, WM, WN, EPI_RES_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_RES_F32) epilogue_fast<BM, BN, WM, WN, EPI_RES_F32>(p, acc, m0, n0, wm, wn, lane, bz);
+  else epilogue_generic<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
+}
+
+// STAGES-deep LDS ring, prefetch distance STAGES-1; waits are counted (vmcnt = loads of the
+// stages allowed to stay in flight) and the barrier is a raw s_barrier, so in-flight LDS-DMA
+// survives it (a __syncthreads() would drain vmcnt(0)).
+template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
+  constexpr int NW = WM * WN;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int PD = STAGES - 1;                          // prefetch distance (K-steps)
+  constexpr int LPS = BM / 8 / NW + BN / 8 / NW;          // LDS-DMA instructions per stage per wave
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
+  const int lane = lane_id();
+  const int wave = wave_id_uniform();
+  const int wm = wave / WN, wn = wave % WN;
+  const int bz = blockIdx.z;
+  // XCD-aware bijective remap of the linear tile id
+  const int nwg = p.tiles_mn, bid = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = bid % 8;
+  const int tid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  int mt, nt;
+  tile_coords(tid, p, mt, nt);
+  const int n0 = nt * BN, m0 = mt * BM;
+
+  const bf16* A = p.A + bz * p.sA;
+  const bf16* B = p.B + bz * p.sB;
+  const int K = p.K;
+  const int nk = (K + BK - 1) / BK;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf, int kt) {
+    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* Bs = As + A_BYTES;
+    const int k0 = kt * BK;
+    if (AT) stage_mn<BM, NW>(A + (int64_t)k0 * p.lda + m0, p.lda, p.M - m0, K - k0, As, wave, lane);
+    else    stage_k<BM, NW>(A + (int64_t)m0 * p.lda + k0, p.lda, p.M - m0, K - k0, As, wave, lane);
+    if (BT) stage_mn<BN, NW>(B + (int64_t)k0 * p.ldb + n0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
+    else    stage_k<BN, NW>(B + (int64_t)n0 * p.ldb + k0, p.ldb, p.N - n0, K - k0, Bs, wave, lane);
+  };
+
+  for (int s = 0; s < PD; ++s)
+    if (s < nk) stage(s, s);
+  if (nk >= PD) wait_vm_lgkm0<(PD - 1) * LPS>();     // stage 0 landed, later ones may fly
+  else wait_vm_lgkm0<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % STAGES;
+    const int nxt = (kt + PD) % STAGES;
+    const char* As = smem + cur * (A_BYTES + B_BYTES);
+    const char* Bs = As + A_BYTES;
+    if constexpr (AT || BT) {
+      // transposed (ds_read_b64_tr_b16) reads: fetch both k-halves BEFORE the next stage's
+      // LDS-DMA is issued, else the compiler cannot prove they do not alias the DMA and
+      // drains vmcnt(0) mid-step (the whole load latency exposed every K-step)
+      bf16x8 a[2][FM], b[2][FN];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int ni = 0; ni < FN; ++ni)
+          b[kk][ni] = BT ? frag_mn<BN>(Bs, wn * (BN / WN) + ni * 16, kk, lane)
+                         : frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+          a[kk][mi] = AT ? frag_mn<BM>(As, wm * (BM / WM) + mi * 16, kk, lane)
+                         : frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
+      }
+      if (kt + PD < nk) stage(nxt, kt + PD);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < FN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][ni], a[kk][mi], acc[mi][ni], 0, 0, 0);
+    } else {
+      if (kt + PD < nk) stage(nxt, kt + PD);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 a[FM], b[FN];
+#pragma unroll
+        for (int ni = 0; ni < FN; ++ni) b[ni] = frag_k(Bs, wn * (BN / WN) + ni * 16, kk, lane);
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi) a[mi] = frag_k(As, wm * (BM / WM) + mi * 16, kk, lane);
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < FN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    // stage kt+1 must have landed; stages kt+2 .. kt+PD (when issued) may stay in flight
+    if (kt + PD < nk) wait_vm_lgkm0<(PD - 1) * LPS>();
+    else wait_vm_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+
+  epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ping-pong 256x256 kernel for K-major A and B (the forward X·Wᵀ of every Linear).
+//
+// 8 waves as 2 (rows) x 4 (cols), each wave owns 128x64 of C = 4 quadrants of 64x32.  A K-tile
+// (BK = 64) is consumed in 4 phases, one quadrant per phase (16 MFMAs):
+//   q(0,0): read A-half 0 + B-quarter 0    q(0,1): read B-quarter 1
+//   q(1,1): read A-half 1                  q(1,0): read B-quarter 0 again
+// LDS = 2 buffers (even / odd K-tile) x 4 regions of 16 KiB:
+//   A-half h    : rows  wr*128 + h*64 + [0,64)  for wr = 0,1   (the rows quadrant-row h reads)
+//   B-quarter q : cols  wc*64  + q*32 + [0,32)  for wc = 0..3  (the cols quadrant-col q reads)
+// so each region's last read in a K-tile is one phase (A-h0: 1, B-q1: 2, A-h1: 3, B-q0: 4), and
+// every phase restages exactly one region (2 LDS-DMA per lane) for the K-tile two ahead in the
+// same buffer, one phase after that region's last read (reads are retired by lgkmcnt(0) before
+// the barrier that ends the reading section).  Waits: vmcnt(6) at phases 4 and 8 = three
+// regions left in flight across the barrier (raw s_barrier, never __syncthreads()).
+// The two wave rows run one barrier apart (wave-row 1 takes an extra barrier up front): on each
+// SIMD (waves w and w+4) one wave issues its 16 MFMAs while the other issues LDS reads and DMA.
+// ---------------------------------------------------------------------------------------------
+constexpr int PP_REGION = 16384;
+
+// Stage one 16-KiB region (128 source rows x 64 k) with 2 LDS-DMA per lane; region row R maps to
+// source row (R >> S) * GS + off + (R & (2^S - 1)).  128-B rows, chunk c of row R at c ^ (R & 7).
+template <int S, int GS>
+__device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_left, int k_left, int off,
+                                         char* region, int wave, int lane) {
+  const auto rs = make_rsrc(base);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pce = wave + 8 * i;
+    const int R = pce * 8 + (lane >> 3);
+    const int row = (R >> S) * GS + off + (R & ((1 << S) - 1));
+    const int c = (lane & 7) ^ (R & 7);
+    const bool ok = (row < rows_left) && (c * 8 < k_left);
+    const uint32_t o = ok ? (uint32_t)(((int64_t)row * ld + c * 8) * 2) : TW_OOB;
+    buf_load_lds16(rs, region + pce * 1024, o);
+  }
+}
+
+// Persistent form: gridDim.x (a multiple of 8, <= CUs) workgroups; workgroup b takes the tiles
+// of virtual block ids b, b + G, b + 2G, ... (G = gridDim.x), each mapped through the same
+// XCD-aware bijective remap as a one-tile-per-block launch, so an XCD keeps walking its own
+// contiguous chunk.  The K-tile stream is continuous across tiles (nk rounded up to even; the
+// pad K-tile stages zeros), so the next tile's first K-tiles are already in flight while the
+// finished tile's epilogue runs (between phases, beside the other wave-row's MFMAs).
+__device__ __forceinline__ bool pp_tile(const GemmP& p, int i, int& m0, int& n0, int& bz) {
+  const int vb = blockIdx.x + gridDim.x * i;
+  if (vb >= p.tiles_total) return false;
+  const int nwg = p.tiles_total;
+  const int q = nwg / 8, rr = nwg % 8, xcd = vb % 8;
+  const int tid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + vb / 8;
+  bz = tid / p.tiles_mn;
+  int mt, nt;
+  tile_coords(tid - bz * p.tiles_mn, p, mt, nt);
+  m0 = mt * 256;
+  n0 = nt * 256;
+  return true;
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_REGION];
+  const int lane = lane_id();
+  const int wave = wave_id_uniform();
+  const int wm = wave >> 2, wn = wave & 3;
+  const int K = p.K, nk = (K + BK - 1) / BK, nke = (nk + 1) & ~1;
+  const int G = gridDim.x;
+  const int my_tiles = ((int)blockIdx.x < p.tiles_total) ? (p.tiles_total - (int)blockIdx.x + G - 1) / G : 0;
+  const int total = my_tiles * nke;                       // K-tiles this workgroup consumes
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // region r of buffer b: 0,1 = A-half 0,1; 2,3 = B-quarter 0,1.  K-tile g of the stream goes to
+  // buffer g & 1.  Tile state is carried incrementally (one pp_tile() per tile); a K-tile past
+  // the stream or the pad K-tile stages zeros, keeping the vmcnt counts uniform.
+  // (plain scalars, no struct: a struct select here is promoted to LDS by the compiler, and any
+  // LDS access it cannot disambiguate from the DMA costs a vmcnt(0) drain)
+  auto tile_info = [&](int i, int& m0, int& n0, int& bz, int& kl) {
+    const bool live = i < my_tiles && pp_tile(p, i, m0, n0, bz);
+    if (!live) { m0 = 0; n0 = 0; bz = 0; }
+    kl = live ? K : 0;                       // K extent seen by the stager (0: stage zeros)
+  };
+  auto reg = [&](int b, int r) -> char* { return smem + (b * 4 + r) * PP_REGION; };
+  auto stage = [&](int m0, int n0, int bz, int kl, int kt, int buf, int r) {
+    const int k_left = kl - kt * BK;
+    if (r < 2)
+      pp_stage<6, 128>(p.A + bz * p.sA + (int64_t)m0 * p.lda + kt * BK, p.lda, p.M - m0, k_left, r * 64,
+                       reg(buf, r), wave, lane);
+    else
+      pp_stage<5, 64>(p.B + bz * p.sB + (int64_t)n0 * p.ldb + kt * BK, p.ldb, p.N - n0, k_left, (r - 2) * 32,
+                      reg(buf, r), wave, lane);
+  };
+
+  bf16x8 a[2][4], bb[2][2];
+  auto rdA = [&](int b, int h) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[kk][mi] = frag_k(reg(b, h), wm * 64 + mi * 16, kk, lane);
+  };
+  auto rdB = [&](int b, int qq) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bb[kk][ni] = frag_k(reg(b, 2 + qq), wn * 32 + ni * 16, kk, lane);
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mma = [&](int qm, int qn) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[qm * 4 + mi][qn * 2 + ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[kk][ni], a[kk][mi], acc[qm * 4 + mi][qn * 2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+
+  // prologue: K-tile 0 whole into buffer 0, K-tile 1 without B-quarter 0 into buffer 1
+  int cm, cn, cb, ck;                        // current tile: m0, n0, batch, K extent
+  tile_info(0, cm, cn, cb, ck);
+  int kt = 0, ti = 0;
+  stage(cm, cn, cb, ck, 0, 0, 0); stage(cm, cn, cb, ck, 0, 0, 1);
+  stage(cm, cn, cb, ck, 0, 0, 2); stage(cm, cn, cb, ck, 0, 0, 3);
+  stage(cm, cn, cb, ck, 1, 1, 0); stage(cm, cn, cb, ck, 1, 1, 3); stage(cm, cn, cb, ck, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  sync();
+  if (wm == 1) sync();                       // stagger the wave rows by one barrier
+
+  for (int g = 0; g < total; g += 2) {
+    // K-tiles g, g+1 = (cur, kt), (cur, kt+1); g+2, g+3 = (nxt, k2), (nxt, k2+1)
+    const bool last = kt + 2 >= nke;
+    int nm = cm, nn = cn, nb = cb, nkl = ck, k2 = kt + 2;
+    if (last) {
+      tile_info(ti + 1, nm, nn, nb, nkl);
+      k2 = 0;
+    }
+    // even K-tile g from buffer 0
+    rdB(0, 0); rdA(0, 0); stage(cm, cn, cb, ck, kt + 1, 1, 2);  mma(0, 0);
+    rdB(0, 1);            stage(nm, nn, nb, nkl, k2, 0, 0);     mma(0, 1);
+    rdA(0, 1);            stage(nm, nn, nb, nkl, k2, 0, 3);     mma(1, 1);
+    rdB(0, 0);            stage(nm, nn, nb, nkl, k2, 0, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");            mma(1, 0);
+    // odd K-tile g+1 from buffer 1
+    rdB(1, 0); rdA(1, 0); stage(nm, nn, nb, nkl, k2, 0, 2);     mma(0, 0);
+    rdB(1, 1);            stage(nm, nn, nb, nkl, k2 + 1, 1, 0); mma(0, 1);
+    rdA(1, 1);            stage(nm, nn, nb, nkl, k2 + 1, 1, 3); mma(1, 1);
+    rdB(1, 0);            stage(nm, nn, nb, nkl, k2 + 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");            mma(1, 0);
+    if (last) {                                                 // tile finished
+      if (!(p.flags & 4096) || acc[0][0][0] != acc[0][0][0])    // 4096: diagnostic, skip epilogue
+        epilogue<256, 256, 2, 4>(p, acc, cm, cn, wm, wn, lane, cb);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++ti;
+    }
+    cm = nm; cn = nn; cb = nb; ck = nkl;
+    kt = k2;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // no LDS-DMA may outlive the block
+  if (wm == 0) sync();                       // balance the stagger barrier
+}
+
 template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
 void launch(GemmP p, int batch, hipStream_t stream) {
   p.tiles_n = (p.N + BN - 1) / BN;
@@ -367,9 +714,52 @@ void launch(GemmP p, int batch, hipStream_t stream) {
                      stream, p);
 }
 
+// Host: the specialised epilogue a call qualifies for (alignment for 16-B vectors included).
+int pick_epilogue(const GemmP& p, int batch) {
+  const int f = p.flags & 0xff;
+  auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  const bool c8 = (p.ldc % 8) == 0 && (batch == 1 || (p.sC % 8) == 0) && a16(p.C);
+  const bool c4 = (p.ldc % 4) == 0 && (batch == 1 || (p.sC % 4) == 0) && a16(p.C);
+  const bool b4 = !(f & F_BIAS) || ((uintptr_t)p.bias & 7) == 0;
+  if (!b4) return EPI_GENERIC;
+  if ((f & ~(F_BIAS | F_ROUND)) == 0) {
+    if (p.c_dtype == TW_BF16 && c8) return EPI_STORE_BF16;
+    if (p.c_dtype == TW_F32 && c4) return EPI_STORE_F32;
+    return EPI_GENERIC;
+  }
+  if ((f & ~(F_BIAS | F_AUX_OUT)) == (F_ROUND | F_GELU) && p.c_dtype == TW_BF16 && c8) {
+    if (!(f & F_AUX_OUT)) return EPI_GELU;
+    const bool x8 = (p.ldaux % 8) == 0 && (batch == 1 || (p.sAux % 8) == 0) && a16(p.aux);
+    return x8 ? EPI_GELU_AUX : EPI_GENERIC;
+  }
+  if ((f & ~(F_BIAS | F_ROUND)) == F_RES && p.res_mod == 0 && p.res_dtype == p.c_dtype) {
+    if (p.c_dtype == TW_BF16 && c8 && (p.ldr % 8) == 0 && (batch == 1 || (p.sR % 8) == 0) && a16(p.res))
+      return EPI_RES_BF16;
+    if (p.c_dtype == TW_F32 && c4 && (p.ldr % 4) == 0 && (batch == 1 || (p.sR % 4) == 0) && a16(p.res))
+      return EPI_RES_F32;
+  }
+  return EPI_GENERIC;
+}
+
+void launch_pp(GemmP p, int batch, hipStream_t stream) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n >= 8 ? n : 8;
+  }();
+  p.tiles_n = (p.N + 255) / 256;
+  p.tiles_mn = p.tiles_n * ((p.M + 255) / 256);
+  p.tiles_total = p.tiles_mn * batch;
+  int grid = p.tiles_total <= cus ? p.tiles_total : (cus & ~7);
+  if (p.flags & 8192) grid = p.tiles_total;   // diagnostic: one tile per workgroup
+  hipLaunchKernelGGL(gemm_pp_kernel, dim3(grid), dim3(512), 0, stream, p);
+}
+
 template <bool AT, bool BT>
 void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
-  if (tile == 256) launch<AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
+  if (tile == 2562 && !AT && !BT) launch_pp(p, batch, stream);
+  else if (tile == 256) launch<AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
   else if (tile == 2561) launch<AT, BT, 256, 128, 4, 2, 3>(p, batch, stream);
   else launch<AT, BT, 128, 128, 2, 2, 2>(p, batch, stream);
 }
@@ -398,19 +788,26 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   p.sA = sA; p.sB = sB; p.sC = sC; p.alpha = alpha; p.bias = (const bf16*)bias;
   p.res = res; p.ldr = ldr; p.sR = sR; p.res_dtype = res_dtype; p.res_mod = res_mod;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux; p.c_dtype = c_dtype; p.flags = flags;
+  static const int env_group = [] {
+    const char* e = getenv("TW_GEMM_GROUP_M");   // A/B sweeps only (tools/bench_gemm.py)
+    return e ? atoi(e) : 0;
+  }();
+  p.group_m = env_group > 0 ? env_group : 1;
+  p.epi = pick_epilogue(p, batch);
   // 256x256 tiles (8 waves) when the problem has enough tiles to fill the chip, else 128x128
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
-  const int64_t t2561 = (int64_t)((M + 255) / 256) * ((N + 127) / 128) * batch;
-  // measured crossovers (tools/bench_gemm.py, r01): the 3-stage 256x128 ring wins by 8-12% on
-  // the K<=4096 NN/NT shapes; long-K reductions (dW, dX of the vocab head) keep the 2-stage
-  // 256x256 tile, small grids the 128x128 one.
+  // measured crossovers (tools/bench_gemm.py, r01, specialised epilogues): the persistent 256x256
+  // ping-pong kernel wins every large K-major/K-major shape (1.05-1.27 PFLOP/s); the 2-stage
+  // 256x256 tile the large transposed ones; 128x128 the small grids (< ~1000 256-tiles).  The
+  // 256x128 3-stage ring is kept as a forced variant only.
   int tile = (t256 >= 1000 && K >= 256) ? 256 : 128;
-  if (!a_trans && K >= 256 && K <= 4096 && t2561 >= 1500) tile = 2561;
+  if (tile == 256 && !a_trans && !b_trans) tile = 2562;
   if (flags & 256) tile = 128;        // forced tile (benchmarking / A-B comparisons)
   if (flags & 512) tile = 256;
   if (flags & 1024) tile = 2561;      // 256x128, 3-stage ring
-  const int64_t ntiles = tile == 256 ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-  if (ntiles > 0x7fffffff || batch > 65535) return TW_EINVAL;
+  if (flags & 2048) tile = 2562;      // 256x256 ping-pong (K-major A and B only)
+  const int64_t ntiles = (tile == 256 || tile == 2562) ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
   if (!a_trans && !b_trans) dispatch<false, false>(p, batch, stream, tile);
   else if (!a_trans && b_trans) dispatch<false, true>(p, batch, stream, tile);
   else if (a_trans && !b_trans) dispatch<true, false>(p, batch, stream, tile);

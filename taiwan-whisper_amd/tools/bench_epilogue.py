@@ -23,7 +23,7 @@ def t(fn, rounds=5, reps=3):
     return sorted(out)[len(out) // 2]
 
 
-VARIANTS = (("t256", ops.GEMM_TILE256), ("s3", ops.GEMM_TILE256x128))
+VARIANTS = (("t256", ops.GEMM_TILE256), ("s3", ops.GEMM_TILE256x128), ("pp", ops.GEMM_TILE256PP))
 
 
 def main():

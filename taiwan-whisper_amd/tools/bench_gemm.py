@@ -8,7 +8,7 @@ import torch
 
 from tw import ops
 
-VARIANTS = (("t128", 256), ("t256", 512), ("t256x128s3", 1024))
+VARIANTS = (("t128", 256), ("t256", 512), ("s3", 1024), ("pp", 2048))
 SHAPES = [  # (name, M, N, K, a_trans, b_trans)
     ("enc qkv", 96000, 3840, 1280, 0, 0), ("enc out", 96000, 1280, 1280, 0, 0),
     ("enc fc1", 96000, 5120, 1280, 0, 0), ("enc fc2", 96000, 1280, 5120, 0, 0),

@@ -15,7 +15,7 @@ import sys
 from collections import defaultdict
 
 FAMILIES = {
-    "gemm_nn": r"gemm_kernel<false, false",
+    "gemm_nn": r"gemm_kernel<false, false|gemm_pp_kernel",
     "gemm_nt": r"gemm_kernel<false, true",
     "gemm_tt": r"gemm_kernel<true, true",
     "attn_fwd": r"attn_fwd_kernel",

@@ -85,6 +85,54 @@ def test_gemm_epilogues():
     assert (C4.float().cpu() - x.grad).abs().max() <= 2 ** -7 * x.grad.abs().max() + 1e-6
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 264, 200), (520, 600, 1344), (1000, 784, 1280), (256, 256, 64)])
+def test_gemm_forced_tiles_bit_identical(M, N, K):
+    """Every tile variant (128², 256², 256x128 3-stage ring, 256² ping-pong) accumulates each output
+    in the same K order, so outputs must agree bit for bit; ragged M/N/K and an odd K-tile count
+    (1344 = 21 x 64) exercise the OOB-zero staging and the ping-pong's pad K-tile.  Each epilogue
+    kind (bf16 / f32 store, bias+GELU with pre-activation aux, in-place bf16 and f32 residual) is
+    also checked against an fp64 reference (tolerance: one bf16 ulp of the largest value)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias, res = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    acc = bf(A).double() @ bf(W).double().T
+    y = bf((acc + bf(bias).double()).float()).float()                  # bf16(Linear) as autocast
+    refs = {"f32": acc.float(), "bf16": y, "gelu": bf(torch.nn.functional.gelu(y)).float(), "aux": y,
+            "res_bf16": bf(y + bf(res).float()).float(), "res_f32": y + res}
+    outs = {}
+    for name, f in (("t128", ops.GEMM_TILE128), ("t256", ops.GEMM_TILE256), ("s3", ops.GEMM_TILE256x128),
+                    ("pp", ops.GEMM_TILE256PP)):
+        o = {}
+        C = torch.full((M, N), float("nan"), dtype=torch.float32, device=DEV)
+        ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N, flags=f)
+        o["f32"] = C
+        Cb = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, Cb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, flags=ops.GEMM_ROUND | f)
+        o["bf16"] = Cb
+        Cg, aux = torch.empty_like(Cb), torch.empty_like(Cb)
+        ops.gemm(Ad, Wd, Cg, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, aux=aux, ldaux=N,
+                 flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT | f)
+        o["gelu"], o["aux"] = Cg, aux
+        rb = bf(res).to(DEV)                                          # in-place bf16 residual stream
+        ops.gemm(Ad, Wd, rb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rb, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_bf16"] = rb
+        rf = res.clone().to(DEV)                                      # in-place fp32 residual stream
+        ops.gemm(Ad, Wd, rf, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rf, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_f32"] = rf
+        torch.cuda.synchronize()
+        outs[name] = {k: v.float().cpu() for k, v in o.items()}
+    for kind, ref in refs.items():
+        got = outs["t128"][kind]
+        if kind == "f32":
+            assert rel_err(got, acc) < 1e-5
+        else:
+            assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max(), kind
+        for name in outs:
+            assert torch.equal(outs[name][kind], got), (name, kind)
+
+
 def test_gemm_batched_strided_view():
     """conv2-style zero-copy im2col: A rows = 3 consecutive rows of a padded buffer (lda = 2*C)."""
     from tw import ops
