@@ -209,7 +209,8 @@ def test_attention_fwd_bwd(B, H, Tq, Tk, causal):
     sh = lambda t, T: t.float().view(B, T, H, 64).transpose(1, 2)
     ref, ref_lse = ref_attn(sh(q, Tq), sh(k, Tk), sh(v, Tk), causal, scale)
     ref = ref.transpose(1, 2).reshape(B * Tq, d)
-    assert (o.float().cpu() - ref).abs().max() < 2e-2 * ref.abs().max()
+    err = (o.float().cpu() - ref).abs()
+    assert err.max() < 1e-2 * ref.abs().max() and err.mean() < 1e-3 * ref.abs().max()
     assert (lse.cpu().view(B, H, Tq) - ref_lse).abs().max() < 1e-3
     # backward vs fp64 autograd on the same bf16 inputs
     qq, kk, vv = (sh(t, T).double().requires_grad_(True) for t, T in ((q, Tq), (k, Tk), (v, Tk)))
