@@ -111,6 +111,23 @@ int tw_shift_tokens_right(const int64_t* labels, int64_t* out, int B, int T, int
                           tw_stream_t stream);
 int tw_count_valid(const int64_t* labels, int64_t n, int* out, tw_stream_t stream);
 
+/* Greedy decoding with a KV cache (generate_step run_distillation.py:1580-1584,
+ * run_pseudo_labelling.py:917-922; HF generation_whisper.py greedy loop, per-step attention of
+ * modeling_whisper.py:265-350 with past_key_values).
+ * tw_decode_attn: one query row per (batch b, head h): O[b][h*64..] = softmax(scale * q.K^T) V over
+ * the first Tk key rows; q at q + b*sqb + h*64, key j at k + b*skb + j*ldk + h*64 (v alike),
+ * output at o + b*sob + h*64 (bf16).  head_dim 64, Tk <= 2048.
+ * tw_greedy_select: HF SuppressTokens / SuppressTokensAtBegin (logits_process.py) + argmax
+ * (lowest id on ties) over the first V logits of each bf16 row; suppress_bits / begin_bits are
+ * V-bit masks (begin applied when apply_begin); rows with done[b] != 0 emit eos; the token is
+ * written to ids[b*ld_ids + col] and next_ids[b], and done[b] |= (token == eos). */
+int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v, int64_t ldv,
+                   int64_t svb, void* o, int64_t sob, int B, int H, int Tk, int head_dim, float scale,
+                   tw_stream_t stream);
+int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                     const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
+                     int64_t ld_ids, int col, int64_t* next_ids, tw_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,190 @@
+// Greedy decoding with a KV cache (generate_step, run_distillation.py:1580-1584;
+// HF generation_whisper.py greedy path; logits processors logits_process.py SuppressTokens /
+// SuppressTokensAtBegin).
+//
+//  * tw_decode_attn: one query row per (batch, head) against Tk cached keys — the decoder's
+//    self-attention over its cache (Tk = t + 1) and cross-attention over the encoder frames
+//    (Tk = 1500).  HBM-bound: every K and V row is read once, 16 B per lane (8 lanes per
+//    128-B head row), scores kept in LDS, exact two-pass softmax (max, then exp / sum / P·V).
+//  * tw_greedy_select: per batch row, argmax over the vocabulary of the fp32 view of the
+//    logits with suppressed ids masked (bitmask; the begin-suppress set only at the first
+//    generated step), finished rows forced to eos (= pad), token written to the id matrix and
+//    to the next step's input vector, finished flag updated.  Ties resolve to the lowest id
+//    (torch.argmax).
+#include "common.h"
+
+namespace {
+
+constexpr int DA_THREADS = 256;
+constexpr int DA_MAX_TK = 2048;
+
+struct DecP {
+  const bf16* q; int64_t sqb;
+  const bf16* k; int64_t ldk, skb;
+  const bf16* v; int64_t ldv, svb;
+  bf16* o; int64_t sob;
+  int H, Tk;
+  float c;        // scale * log2(e)
+};
+
+// lane = (key slot ks = lane >> 3, 16-B chunk ch = lane & 7); a wave covers 8 keys per step
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
+  __shared__ float sc[DA_MAX_TK];
+  __shared__ float red[DA_THREADS / 64][64];
+  __shared__ float red_l[DA_THREADS / 64];
+  __shared__ float red_m[DA_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ks = lane >> 3, ch = lane & 7;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const bf16* qb = p.q + b * p.sqb + h * 64 + ch * 8;
+  const bf16* kb = p.k + b * p.skb + h * 64 + ch * 8;
+  const bf16* vb = p.v + b * p.svb + h * 64 + ch * 8;
+  float qv[8];
+  {
+    const bf16x8 t = *(const bf16x8*)qb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[j] = bf2f(t[j]);
+  }
+  // pass 1: scores (log2 domain) -> LDS, running max
+  float mx = -INFINITY;
+  for (int k0 = wave * 8; k0 < p.Tk; k0 += DA_THREADS / 8) {
+    const int key = k0 + ks;
+    float s = 0.f;
+    if (key < p.Tk) {
+      const bf16x8 t = *(const bf16x8*)(kb + (int64_t)key * p.ldk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = fmaf(qv[j], bf2f(t[j]), s);
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (key < p.Tk) {
+      s *= p.c;
+      if (ch == 0) sc[key] = s;
+      mx = fmaxf(mx, s);
+    }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red_m[wave] = mx;
+  __syncthreads();
+  float m = red_m[0];
+#pragma unroll
+  for (int w = 1; w < DA_THREADS / 64; ++w) m = fmaxf(m, red_m[w]);
+  // pass 2: p = exp2(s - m), l = sum p, o = sum p * V
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float l = 0.f;
+  for (int k0 = wave * 8; k0 < p.Tk; k0 += DA_THREADS / 8) {
+    const int key = k0 + ks;
+    if (key < p.Tk) {
+      const float pe = __builtin_amdgcn_exp2f(sc[key] - m);
+      const bf16x8 t = *(const bf16x8*)(vb + (int64_t)key * p.ldv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaf(pe, bf2f(t[j]), o[j]);
+      if (ch == 0) l += pe;
+    }
+  }
+  // reduce over the 8 key slots of the wave (lanes ch, ch+8, ..., ch+56), then over waves
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    o[j] += __shfl_xor(o[j], 8, 64);
+    o[j] += __shfl_xor(o[j], 16, 64);
+    o[j] += __shfl_xor(o[j], 32, 64);
+  }
+  l = wave_sum(l);
+  if (ks == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][ch * 8 + j] = o[j];
+  }
+  if (lane == 0) red_l[wave] = l;
+  __syncthreads();
+  if (tid < 64) {
+    float acc = 0.f, lt = 0.f;
+#pragma unroll
+    for (int w = 0; w < DA_THREADS / 64; ++w) {
+      acc += red[w][tid];
+      lt += red_l[w];
+    }
+    p.o[b * p.sob + h * 64 + tid] = f2bf(acc / lt);
+  }
+}
+
+struct SelP {
+  const bf16* logits; int64_t ld;
+  int V;
+  const uint32_t* suppress;   // V-bit mask (nullable)
+  const uint32_t* begin;      // V-bit mask applied when apply_begin (nullable)
+  int apply_begin;
+  int64_t eos;
+  uint8_t* done;
+  int64_t* ids; int64_t ld_ids; int col;
+  int64_t* next;              // [B] next-step input ids
+};
+
+__device__ __forceinline__ bool bit(const uint32_t* m, int v) { return m && ((m[v >> 5] >> (v & 31)) & 1u); }
+
+__global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16* row = p.logits + b * p.ld;
+  float best = -INFINITY;
+  int besti = 0x7fffffff;
+  for (int v = tid; v < p.V; v += 256) {
+    float x = bf2f(row[v]);
+    if (bit(p.suppress, v) || (p.apply_begin && bit(p.begin, v))) x = -INFINITY;
+    if (x > best || (x == best && v < besti)) { best = x; besti = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(besti, o, 64);
+    if (ov > best || (ov == best && oi < besti)) { best = ov; besti = oi; }
+  }
+  if (lane == 0) { bv[wave] = best; bi[wave] = besti; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (bv[w] > best || (bv[w] == best && bi[w] < besti)) { best = bv[w]; besti = bi[w]; }
+    if (besti == 0x7fffffff) besti = 0;            // every logit masked / NaN: id 0 (torch argmax of all -inf)
+    const bool fin = p.done[b] != 0;
+    const int64_t tok = fin ? p.eos : (int64_t)besti;
+    p.ids[b * p.ld_ids + p.col] = tok;
+    p.next[b] = tok;
+    p.done[b] = (fin || tok == p.eos) ? 1 : 0;
+  }
+}
+
+}  // namespace
+
+extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v,
+                              int64_t ldv, int64_t svb, void* o, int64_t sob, int B, int H, int Tk, int head_dim,
+                              float scale, hipStream_t stream) {
+  if (head_dim != 64) return TW_EUNSUPPORTED;
+  if (B <= 0 || H <= 0) return TW_OK;
+  if (Tk <= 0 || Tk > DA_MAX_TK) return TW_EUNSUPPORTED;
+  if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) return TW_EINVAL;
+  if ((sqb | ldk | skb | ldv | svb) & 7) return TW_EINVAL;
+  DecP p;
+  p.q = (const bf16*)q; p.sqb = sqb;
+  p.k = (const bf16*)k; p.ldk = ldk; p.skb = skb;
+  p.v = (const bf16*)v; p.ldv = ldv; p.svb = svb;
+  p.o = (bf16*)o; p.sob = sob;
+  p.H = H; p.Tk = Tk; p.c = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(decode_attn_kernel, dim3(B * H), dim3(DA_THREADS), 0, stream, p);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                                const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
+                                int64_t ld_ids, int col, int64_t* next_ids, hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  if (V <= 0 || ld < V || !done || !ids || !next_ids) return TW_EINVAL;
+  SelP p;
+  p.logits = (const bf16*)logits; p.ld = ld; p.V = V;
+  p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
+  p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
+  hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}

@@ -57,3 +57,28 @@ class WhisperConfig:
 
     def __repr__(self):
         return f"WhisperConfig(d_model={self.d_model}, enc={self.encoder_layers}, dec={self.decoder_layers})"
+
+
+GEN_DEFAULTS = dict(
+    decoder_start_token_id=50258, eos_token_id=50257, pad_token_id=50257, bos_token_id=50257,
+    no_timestamps_token_id=50363, max_length=448, num_beams=1, suppress_tokens=[], begin_suppress_tokens=[220, 50257],
+    is_multilingual=True, lang_to_id={}, task_to_id={"transcribe": 50359, "translate": 50358},
+)
+
+
+class GenerationConfig(dict):
+    """`generation_config.json` as a dict (round-trips unchanged) with HF-style attribute access and
+    the Whisper defaults for keys the file lacks (HF generation_whisper.py reads these fields)."""
+
+    def __getattr__(self, name):
+        if name in self:
+            return self[name]
+        if name in GEN_DEFAULTS:
+            return copy.deepcopy(GEN_DEFAULTS[name])
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        self[name] = value
+
+    def to_dict(self):
+        return copy.deepcopy(dict(self))

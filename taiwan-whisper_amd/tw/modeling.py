@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .config import WhisperConfig
+from .config import GenerationConfig, WhisperConfig
 
 F = ops
 
@@ -292,7 +292,7 @@ class WhisperForConditionalGeneration:
         gp = os.path.join(path, "generation_config.json")
         if os.path.exists(gp):
             with open(gp) as f:
-                m.generation_config = json.load(f)
+                m.generation_config = GenerationConfig(json.load(f))
         return m
 
     def save_pretrained(self, path):
@@ -303,7 +303,7 @@ class WhisperForConditionalGeneration:
         save_file(sd, os.path.join(path, "model.safetensors"), metadata={"format": "pt"})
         if self.generation_config is not None:
             with open(os.path.join(path, "generation_config.json"), "w") as f:
-                json.dump(self.generation_config, f, indent=2)
+                json.dump(dict(self.generation_config), f, indent=2)
 
     # ------------------------------------------------------------------ training layout
     def set_trainable(self, prefix, flag):
@@ -570,6 +570,11 @@ class WhisperForConditionalGeneration:
                              logits_padded=lp)
 
     forward = __call__
+
+    def generate(self, input_features=None, **kw):
+        """Greedy decoding with a KV cache (tw/generation.py)."""
+        from .generation import generate
+        return generate(self, input_features, **kw)
 
 
 # =============================================================================================

@@ -252,3 +252,42 @@ def gelu_bwd(g, pre, out):
     assert pre.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and g.numel() == pre.numel() == out.numel()
     call("tw_gelu_bwd", g.data_ptr(), _dt(g), pre.data_ptr(), out.data_ptr(), g.numel(), _stream())
     return out
+
+
+# ----------------------------------------------------------------------------- greedy decode (A12)
+def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale):
+    """One query row per (b, h) over the first Tk cached key rows (include/tw_hip.h)."""
+    hd = 64
+    for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
+        assert t.dtype == torch.bfloat16, nm
+    _need(q, (B - 1) * sqb + H * hd, "decode q")
+    _need(k, (B - 1) * skb + (Tk - 1) * ldk + H * hd, "decode k")
+    _need(v, (B - 1) * svb + (Tk - 1) * ldv + H * hd, "decode v")
+    _need(o, (B - 1) * sob + H * hd, "decode o")
+    call("tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb, o.data_ptr(), sob,
+         B, H, Tk, hd, float(scale), _stream())
+    return o
+
+
+def token_bitmask(ids, V, device):
+    """V-bit uint32 mask (as int32 storage) with the given token ids set."""
+    words = torch.zeros((V + 31) // 32, dtype=torch.int64)
+    for i in ids:
+        i = int(i)
+        if 0 <= i < V:
+            words[i >> 5] |= 1 << (i & 31)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
+    return words.to(torch.int32).to(device)
+
+
+def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids):
+    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
+    assert done.dtype == torch.uint8
+    _need(logits, (B - 1) * ld + V, "greedy logits")
+    _need(ids, (B - 1) * ids.stride(0) + col + 1, "greedy ids")
+    _need(done, B, "greedy done"); _need(next_ids, B, "greedy next")
+    for m, nm in ((suppress_bits, "suppress"), (begin_bits, "begin")):
+        if m is not None:
+            _need(m, (V + 31) // 32, f"greedy {nm} mask")
+    call("tw_greedy_select", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
+         int(eos), done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _stream())
