@@ -114,19 +114,29 @@ int tw_count_valid(const int64_t* labels, int64_t n, int* out, tw_stream_t strea
 /* Greedy decoding with a KV cache (generate_step run_distillation.py:1580-1584,
  * run_pseudo_labelling.py:917-922; HF generation_whisper.py greedy loop, per-step attention of
  * modeling_whisper.py:265-350 with past_key_values).
+ * Position-independent steps (for graph capture): the step index t lives in device memory
+ * (t_dev) and is read by the kernels that depend on it; tw_step_advance adds `by` to it.
  * tw_decode_attn: one query row per (batch b, head h): O[b][h*64..] = softmax(scale * q.K^T) V over
- * the first Tk key rows; q at q + b*sqb + h*64, key j at k + b*skb + j*ldk + h*64 (v alike),
- * output at o + b*sob + h*64 (bf16).  head_dim 64, Tk <= 2048.
+ * the first Tk key rows (Tk += *tk_dev when tk_dev != NULL); q at q + b*sqb + h*64, key j at
+ * k + b*skb + j*ldk + h*64 (v alike), output at o + b*sob + h*64 (bf16).  head_dim 64, Tk <= 2048.
  * tw_greedy_select: HF SuppressTokens / SuppressTokensAtBegin (logits_process.py) + argmax
  * (lowest id on ties) over the first V logits of each bf16 row; suppress_bits / begin_bits are
- * V-bit masks (begin applied when apply_begin); rows with done[b] != 0 emit eos; the token is
- * written to ids[b*ld_ids + col] and next_ids[b], and done[b] |= (token == eos). */
+ * V-bit masks; rows with done[b] != 0 emit eos; the token is written to ids[b*ld_ids + col] and
+ * next_ids[b], and done[b] |= (token == eos).  With t_dev != NULL: col += *t_dev and the begin mask
+ * applies when col == begin_col (apply_begin is ignored).
+ * tw_embed_step: out[b] = tok[ids[b]] + pos[*t_dev] (decoder input embedding of one step).
+ * tw_kv_append: cache[b*sb + (*t_dev)*ld_row + 0..n) = src[b*ld_src + 0..n) (bf16, n % 8 == 0). */
 int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v, int64_t ldv,
-                   int64_t svb, void* o, int64_t sob, int B, int H, int Tk, int head_dim, float scale,
-                   tw_stream_t stream);
+                   int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev, int head_dim,
+                   float scale, tw_stream_t stream);
 int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
                      const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
-                     int64_t ld_ids, int col, int64_t* next_ids, tw_stream_t stream);
+                     int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col, tw_stream_t stream);
+int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
+                  int out_dtype, int B, int D, const int* t_dev, tw_stream_t stream);
+int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n,
+                 const int* t_dev, tw_stream_t stream);
+int tw_step_advance(int* t_dev, int by, tw_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,7 @@ struct DecP {
   const bf16* v; int64_t ldv, svb;
   bf16* o; int64_t sob;
   int H, Tk;
+  const int* tk_dev;  // nullable: effective Tk = *tk_dev + Tk (graph-captured decode steps)
   float c;        // scale * log2(e)
 };
 
@@ -36,6 +37,8 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ks = lane >> 3, ch = lane & 7;
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  if (p.tk_dev) p.Tk += *p.tk_dev;
+  if (p.Tk > DA_MAX_TK) p.Tk = DA_MAX_TK;
   const bf16* qb = p.q + b * p.sqb + h * 64 + ch * 8;
   const bf16* kb = p.k + b * p.skb + h * 64 + ch * 8;
   const bf16* vb = p.v + b * p.svb + h * 64 + ch * 8;
@@ -118,6 +121,8 @@ struct SelP {
   uint8_t* done;
   int64_t* ids; int64_t ld_ids; int col;
   int64_t* next;              // [B] next-step input ids
+  const int* t_dev;           // nullable: col = *t_dev + col, begin mask applied when col == begin_col
+  int begin_col;
 };
 
 __device__ __forceinline__ bool bit(const uint32_t* m, int v) { return m && ((m[v >> 5] >> (v & 31)) & 1u); }
@@ -126,6 +131,10 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
   __shared__ float bv[4];
   __shared__ int bi[4];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (p.t_dev) {
+    p.col += *p.t_dev;
+    p.apply_begin = p.col == p.begin_col;
+  }
   const bf16* row = p.logits + b * p.ld;
   float best = -INFINITY;
   int besti = 0x7fffffff;
@@ -154,14 +163,69 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
   }
 }
 
+// x[b] = tok[ids[b]] + pos[*t_dev]   (decoder input embedding of step t, HF modeling_whisper.py:720-735)
+__global__ void embed_step_kernel(const int64_t* __restrict__ ids, const void* __restrict__ tok, int tok_dtype,
+                                  const void* __restrict__ pos, int pos_dtype, void* __restrict__ out, int out_dtype,
+                                  int D, const int* __restrict__ t_dev) {
+  const int b = blockIdx.x;
+  const int64_t id = ids[b];
+  const int64_t t = *t_dev;
+  for (int e = threadIdx.x; e < D; e += blockDim.x) {
+    const float s = ld_as_f32(tok, tok_dtype, id * D + e) + ld_as_f32(pos, pos_dtype, t * D + e);
+    if (out_dtype == TW_BF16) ((bf16*)out)[(int64_t)b * D + e] = f2bf(s);
+    else ((float*)out)[(int64_t)b * D + e] = s;
+  }
+}
+
+// cache[b][*t_dev][0:n] = src[b][0:n]   (16-B vectors)
+__global__ void kv_append_kernel(const bf16* __restrict__ src, int64_t ld_src, bf16* __restrict__ cache,
+                                 int64_t ld_row, int64_t sb, int n, const int* __restrict__ t_dev) {
+  const int b = blockIdx.y;
+  const int64_t t = *t_dev;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i < n) *(bf16x8*)(cache + b * sb + t * ld_row + i) = *(const bf16x8*)(src + b * ld_src + i);
+}
+
+__global__ void step_advance_kernel(int* t_dev, int by) {
+  if (threadIdx.x == 0) *t_dev += by;
+}
+
 }  // namespace
 
+extern "C" int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype,
+                             void* out, int out_dtype, int B, int D, const int* t_dev, hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  if (!t_dev || D <= 0) return TW_EINVAL;
+  hipLaunchKernelGGL(embed_step_kernel, dim3(B), dim3(256), 0, stream, ids, tok, tok_dtype, pos, pos_dtype, out,
+                     out_dtype, D, t_dev);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n,
+                            const int* t_dev, hipStream_t stream) {
+  if (B <= 0 || n <= 0) return TW_OK;
+  if (!t_dev || (n & 7) || (ld_src & 7) || (ld_row & 7) || (sb & 7) || (((uintptr_t)src | (uintptr_t)cache) & 15))
+    return TW_EINVAL;
+  hipLaunchKernelGGL(kv_append_kernel, dim3((n / 8 + 255) / 256, B), dim3(256), 0, stream, (const bf16*)src, ld_src,
+                     (bf16*)cache, ld_row, sb, n, t_dev);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_step_advance(int* t_dev, int by, hipStream_t stream) {
+  if (!t_dev) return TW_EINVAL;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, stream, t_dev, by);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
 extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v,
-                              int64_t ldv, int64_t svb, void* o, int64_t sob, int B, int H, int Tk, int head_dim,
-                              float scale, hipStream_t stream) {
+                              int64_t ldv, int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev,
+                              int head_dim, float scale, hipStream_t stream) {
   if (head_dim != 64) return TW_EUNSUPPORTED;
   if (B <= 0 || H <= 0) return TW_OK;
-  if (Tk <= 0 || Tk > DA_MAX_TK) return TW_EUNSUPPORTED;
+  if ((!tk_dev && Tk <= 0) || Tk > DA_MAX_TK) return TW_EUNSUPPORTED;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) return TW_EINVAL;
   if ((sqb | ldk | skb | ldv | svb) & 7) return TW_EINVAL;
   DecP p;
@@ -169,7 +233,7 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   p.k = (const bf16*)k; p.ldk = ldk; p.skb = skb;
   p.v = (const bf16*)v; p.ldv = ldv; p.svb = svb;
   p.o = (bf16*)o; p.sob = sob;
-  p.H = H; p.Tk = Tk; p.c = scale * 1.4426950408889634f;
+  p.H = H; p.Tk = Tk; p.tk_dev = tk_dev; p.c = scale * 1.4426950408889634f;
   hipLaunchKernelGGL(decode_attn_kernel, dim3(B * H), dim3(DA_THREADS), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
@@ -177,13 +241,15 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
 
 extern "C" int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
                                 const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
-                                int64_t ld_ids, int col, int64_t* next_ids, hipStream_t stream) {
+                                int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col,
+                                hipStream_t stream) {
   if (B <= 0) return TW_OK;
   if (V <= 0 || ld < V || !done || !ids || !next_ids) return TW_EINVAL;
   SelP p;
   p.logits = (const bf16*)logits; p.ld = ld; p.V = V;
   p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
+  p.t_dev = t_dev; p.begin_col = begin_col;
   hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;

@@ -714,6 +714,101 @@ void launch(GemmP p, int batch, hipStream_t stream) {
                      stream, p);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skinny GEMM for the decode step (M <= 128 rows = the batch of one greedy step, A and B K-major):
+// weight streaming.  One 256-thread workgroup per 16-column slice of W (all M rows), the K range
+// split over the 4 waves; W fragments load straight from HBM (16 B per lane, each W byte read
+// once per step), A fragments from L2 (A is at most 128 x K bf16), MFMA 16x16x32 with swapped
+// operands, the 4 wave partials summed through LDS, then the per-element epilogue (every flag).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float v) {
+  const int flags = p.flags;
+  v *= p.alpha;
+  if (flags & F_BIAS) v += bf2f(p.bias[n]);
+  if (flags & F_ROUND) v = rbf(v);
+  if (flags & F_DGELU) v = rbf(v * gelu_erf_grad(bf2f(p.aux[(int64_t)m * p.ldaux + n])));
+  if (flags & F_GELU) {
+    if (flags & F_AUX_OUT) p.aux[(int64_t)m * p.ldaux + n] = f2bf(v);
+    v = rbf(gelu_erf(v));
+  }
+  if (flags & F_RES) {
+    const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
+    v += ld_as_f32(p.res, p.res_dtype, (int64_t)mr * p.ldr + n);
+  }
+  const int64_t co = (int64_t)m * p.ldc + n;
+  if (flags & F_ACCUM) v += ld_as_f32(p.C, p.c_dtype, co);
+  if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2bf(v);
+  else ((float*)p.C)[co] = v;
+}
+
+template <int MF>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmP p) {
+  __shared__ float part[4][MF * 16][17];
+  const int lane = lane_id(), wave = wave_id_uniform();
+  const int n0 = blockIdx.x * 16;
+  const int li = lane & 15, g = lane >> 4;
+  const int nk = (p.K + 31) / 32;                         // 32-deep k-steps
+  const int per = (nk + 3) / 4;
+  const int k_beg = wave * per, k_end = min(nk, k_beg + per);
+  f32x4 acc[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wrow = n0 + li;
+  const bool wok = wrow < p.N;
+  const bf16* wp = p.B + (int64_t)(wok ? wrow : 0) * p.ldb + 8 * g;
+  const bf16* ap[MF];
+  bool aok[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int m = i * 16 + li;
+    aok[i] = m < p.M;
+    ap[i] = p.A + (int64_t)(aok[i] ? m : 0) * p.lda + 8 * g;
+  }
+  auto ldk = [&](const bf16* base, int ks, bool ok) -> bf16x8 {
+    const int k = ks * 32 + 8 * g;
+    return (ok && k < p.K) ? *(const bf16x8*)(base + ks * 32) : bf16x8{};
+  };
+  int ks = k_beg;
+  for (; ks + 1 < k_end; ks += 2) {                        // two k-steps of loads in flight
+    const bf16x8 w0 = ldk(wp, ks, wok), w1 = ldk(wp, ks + 1, wok);
+    bf16x8 a0[MF], a1[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) { a0[i] = ldk(ap[i], ks, aok[i]); a1[i] = ldk(ap[i], ks + 1, aok[i]); }
+#pragma unroll
+    for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, a0[i], acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, a1[i], acc[i], 0, 0, 0);
+  }
+  if (ks < k_end) {
+    const bf16x8 w0 = ldk(wp, ks, wok);
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, ldk(ap[i], ks, aok[i]), acc[i], 0, 0, 0);
+  }
+  // lane holds C[16i + li][n0 + 4g + r]
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[wave][i * 16 + li][4 * g + r] = acc[i][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < MF * 16 * 16; e += 256) {
+    const int m = e >> 4, c = e & 15, n = n0 + c;
+    if (m < p.M && n < p.N) epi_element(p, m, n, part[0][m][c] + part[1][m][c] + part[2][m][c] + part[3][m][c]);
+  }
+}
+
+void launch_skinny(GemmP p, hipStream_t stream) {
+  const dim3 grid((p.N + 15) / 16);
+  const int mf = (p.M + 15) / 16;
+  switch (mf) {
+    case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, stream, p); break;
+    case 3:
+    case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(256), 0, stream, p); break;
+    default: hipLaunchKernelGGL(gemm_skinny_kernel<8>, grid, dim3(256), 0, stream, p); break;
+  }
+}
+
 // Host: the specialised epilogue a call qualifies for (alignment for 16-B vectors included).
 int pick_epilogue(const GemmP& p, int batch) {
   const int f = p.flags & 0xff;
@@ -808,6 +903,12 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   if (flags & 2048) tile = 2562;      // 256x256 ping-pong (K-major A and B only)
   const int64_t ntiles = (tile == 256 || tile == 2562) ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
+  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && !(flags & (256 | 512 | 1024 | 2048));
+  if (skinny && ((uintptr_t)A & 15) == 0) {
+    launch_skinny(p, stream);                         // decode-step GEMMs: stream W once
+    TW_CHECK_LAUNCH();
+    return TW_OK;
+  }
   if (!a_trans && !b_trans) dispatch<false, false>(p, batch, stream, tile);
   else if (!a_trans && b_trans) dispatch<false, true>(p, batch, stream, tile);
   else if (a_trans && !b_trans) dispatch<true, false>(p, batch, stream, tile);

@@ -38,8 +38,11 @@ SIGNATURES = {
     "tw_gelu_bwd": [P, I32, P, P, I64, P],
     "tw_shift_tokens_right": [P, P, I32, I32, I64, I64, P],
     "tw_count_valid": [P, I64, P, P],
-    "tw_decode_attn": [P, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, I32, I32, F32, P],
-    "tw_greedy_select": [P, I64, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P],
+    "tw_decode_attn": [P, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, I32, P, I32, F32, P],
+    "tw_greedy_select": [P, I64, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P],
+    "tw_embed_step": [P, P, I32, P, I32, P, I32, I32, I32, P, P],
+    "tw_kv_append": [P, I64, P, I64, I64, I32, I32, P, P],
+    "tw_step_advance": [P, I32, P],
 }
 
 STATUS = {1: "invalid argument / shape", 2: "unsupported configuration", 3: "HIP launch error"}

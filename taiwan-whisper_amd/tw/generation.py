@@ -9,15 +9,17 @@ padded with pad (= eos), stop when every row emitted eos or max_length is reache
 value is the generated ids only (transformers >= 5 behaviour, the version in this image).
 
 Device layout (one DecodeSession per batch of clips):
-  * self-attention cache per decoder layer: bf16 [B][T_max][3d] — the fused QKV projection of
-    step t writes q/k/v straight into row t (GEMM ldc = T_max*3d); keys/values 0..t are read
-    in place by tw_decode_attn;
+  * self-attention cache per decoder layer: bf16 [B][T_max][2d] (k | v); the fused QKV projection
+    of a step goes to a [B][3d] staging buffer and tw_kv_append copies k, v to row t; keys /
+    values 0..t are read in place by tw_decode_attn;
   * cross-attention K/V per decoder layer: bf16 [B*1500][2d], projected once from the encoder
     output (k has no bias: the zero-bias segment of the fused KV bias);
   * logits bf16 [B][Vp]; tw_greedy_select applies the suppress masks, takes the argmax, writes
     the token into the id matrix and the next step's input vector, and tracks finished rows.
-Everything runs on the HIP library; the host only sequences launches (and reads the finished
-flags every 8 steps to stop early).
+Everything runs on the HIP library.  The step index lives in device memory (t_dev: embedding
+position, cache row, self-attention length, output column, begin-suppress test), so one step —
+~14 launches per decoder layer + head + select + advance — is captured once into a HIP graph and
+replayed per token; the host reads the finished flags every 8 steps to stop early.
 """
 from __future__ import annotations
 
@@ -27,6 +29,9 @@ from . import ops as F
 
 
 class DecodeSession:
+    """Device state of one greedy decode over a batch; every step is position-independent (the step
+    index lives in `t_dev`), so the whole step is captured once into a HIP graph and replayed."""
+
     def __init__(self, model, enc16: torch.Tensor, B: int, Tk: int, T_max: int):
         cfg = model.config
         self.m, self.B, self.Tk, self.T_max = model, B, Tk, T_max
@@ -34,7 +39,7 @@ class DecodeSession:
         self.H = self.d // 64
         dev = model.device
         d = self.d
-        self.self_kv = [torch.empty(B, T_max, 3 * d, dtype=torch.bfloat16, device=dev)
+        self.self_kv = [torch.empty(B, T_max, 2 * d, dtype=torch.bfloat16, device=dev)
                         for _ in range(cfg.decoder_layers)]
         self.cross_kv = []
         for i in range(cfg.decoder_layers):
@@ -44,36 +49,48 @@ class DecodeSession:
             bkv = model.store.span(model.store.p16, p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
             model._lin(enc16, wkv, bkv, kv)
             self.cross_kv.append(kv)
+        self.t_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.cur = torch.zeros(B, dtype=torch.int64, device=dev)       # this step's input ids
         self.x = torch.empty(B, d, dtype=model.stream_dtype, device=dev)
+        self.y = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
+        self.qkv = torch.empty(B, 3 * d, dtype=torch.bfloat16, device=dev)
         self.o = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
         self.q = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
         self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=torch.bfloat16, device=dev)
         self.logits = torch.empty(B, model.Vp, dtype=torch.bfloat16, device=dev)
+        self.graph = None
 
-    def step(self, tok: torch.Tensor, t: int) -> torch.Tensor:
-        """tok: int64 [B] (device) at position t -> bf16 logits [B, Vp] of position t."""
+    def _ln(self, x, name):
+        m = self.m
+        F.layernorm_fwd(x, m.ln_param(name + ".weight"), m.ln_param(name + ".bias"), self.y)
+        return self.y
+
+    def step(self, select=None):
+        """One decoder step at position *t_dev for input ids `cur`; then t_dev += 1.
+        select = (sup, beg, eos, done, ids, P) runs greedy selection into ids[:, t+1] and cur."""
         m, B, d, H, T_max = self.m, self.B, self.d, self.H, self.T_max
         if m.store.p32 is not None:
-            E, P = m.store.v32("model.decoder.embed_tokens.weight"), m.store.v32("model.decoder.embed_positions.weight")
+            E, Pe = m.store.v32("model.decoder.embed_tokens.weight"), m.store.v32("model.decoder.embed_positions.weight")
         else:
-            E, P = m.store.v16("model.decoder.embed_tokens.weight"), m.store.v16("model.decoder.embed_positions.weight")
-        x, o = self.x, self.o
-        F.embed_fwd(tok, E, P, x, 1, pos_offset=t)
-        sb = T_max * 3 * d
+            E, Pe = m.store.v16("model.decoder.embed_tokens.weight"), m.store.v16("model.decoder.embed_positions.weight")
+        x, o, t_dev = self.x, self.o, self.t_dev
+        F.embed_step(self.cur, E, Pe, x, t_dev, T_max)
+        sb = T_max * 2 * d
         for i in range(m.config.decoder_layers):
             p = f"model.decoder.layers.{i}"
-            # self attention: q/k/v of position t straight into the cache row t
-            y = m._ln(x, p + ".self_attn_layer_norm")
-            cache = self.self_kv[i].view(-1)
+            # self attention: fused QKV -> staging; k, v appended at row t of the cache
+            y = self._ln(x, p + ".self_attn_layer_norm")
             wqkv = m.store.span(m.store.p16, p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight",
                                 (3 * d, d))
             bqkv = m.store.span(m.store.p16, p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,))
-            F.gemm(y, wqkv, cache[t * 3 * d:], B, 3 * d, d, lda=d, ldb=d, ldc=sb, bias=bqkv, flags=F.GEMM_ROUND)
-            F.decode_attn(cache[t * 3 * d:], sb, cache[d:], 3 * d, sb, cache[2 * d:], 3 * d, sb, o, d, B, H, t + 1,
-                          0.125)
+            m._lin(y, wqkv, bqkv, self.qkv)
+            cache = self.self_kv[i]
+            F.kv_append(self.qkv[:, d:], 3 * d, cache, 2 * d, sb, B, 2 * d, t_dev, T_max)
+            F.decode_attn(self.qkv, 3 * d, cache, 2 * d, sb, cache.view(-1)[d:], 2 * d, sb, o, d, B, H, 1, 0.125,
+                          tk_dev=t_dev, tk_max=T_max)
             m._lin(o, m._w16(p + ".self_attn.out_proj.weight"), m._w16(p + ".self_attn.out_proj.bias"), x, res=x)
             # cross attention over the encoder frames
-            y = m._ln(x, p + ".encoder_attn_layer_norm")
+            y = self._ln(x, p + ".encoder_attn_layer_norm")
             m._lin(y, m._w16(p + ".encoder_attn.q_proj.weight"), m._w16(p + ".encoder_attn.q_proj.bias"), self.q)
             kv = self.cross_kv[i]
             F.decode_attn(self.q, d, kv, 2 * d, self.Tk * 2 * d, kv[:, d:], 2 * d, self.Tk * 2 * d, o, d, B, H,
@@ -81,11 +98,23 @@ class DecodeSession:
             m._lin(o, m._w16(p + ".encoder_attn.out_proj.weight"), m._w16(p + ".encoder_attn.out_proj.bias"), x,
                    res=x)
             # MLP
-            y = m._ln(x, p + ".final_layer_norm")
+            y = self._ln(x, p + ".final_layer_norm")
             m._lin(y, m._w16(p + ".fc1.weight"), m._w16(p + ".fc1.bias"), self.h, flags=F.GEMM_ROUND | F.GEMM_GELU)
             m._lin(self.h, m._w16(p + ".fc2.weight"), m._w16(p + ".fc2.bias"), x, res=x)
-        hN = m._ln(x, "model.decoder.layer_norm")
-        return m.lm_head(hN, out=self.logits)
+        hN = self._ln(x, "model.decoder.layer_norm")
+        m.lm_head(hN, out=self.logits)
+        if select is not None:
+            sup, beg, eos, done, ids, P = select
+            F.greedy_select(self.logits, m.Vp, B, m.config.vocab_size, sup, beg, False, eos, done, ids, 1, self.cur,
+                            t_dev=t_dev, begin_col=P)
+        F.step_advance(t_dev)
+
+    def capture(self, select):
+        """Record one selecting step into a HIP graph (nothing executes during capture)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step(select)
+        self.graph = g
 
 
 def _lang_id(gc, language):
@@ -120,7 +149,7 @@ def build_prompt(gc, language=None, task=None, return_timestamps=False):
 @torch.no_grad()
 def generate(model, input_features=None, max_length=None, num_beams=1, return_timestamps=False, language=None,
              task=None, decoder_input_ids=None, max_new_tokens=None, encoder_outputs=None, attention_mask=None,
-             **kw):
+             use_graph=None, **kw):
     from .config import GenerationConfig
     if num_beams not in (None, 1):
         raise NotImplementedError("tw generate: greedy only (num_beams=1, as every reference call site)")
@@ -165,12 +194,19 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     beg = F.token_bitmask(gc.begin_suppress_tokens or [], V, dev)
     sess = DecodeSession(model, enc16, B, Tk, max_length)
     for t in range(P - 1):                                   # prefill the cache with the prompt
-        sess.step(ids[:, t].contiguous(), t)
-    cur = ids[:, P - 1].contiguous()
+        sess.cur.copy_(ids[:, t])
+        sess.step()
+    sess.cur.copy_(ids[:, P - 1])
+    select = (sup, beg, eos, done, ids, P)
+    graph = use_graph if use_graph is not None else True
+    if graph:
+        sess.capture(select)
     t = P - 1
     while t + 1 < max_length:
-        logits = sess.step(cur, t)
-        F.greedy_select(logits, model.Vp, B, V, sup, beg, t + 1 == P, eos, done, ids, t + 1, cur)
+        if graph:
+            sess.graph.replay()
+        else:
+            sess.step(select)
         t += 1
         if (t - P) % 8 == 7 and bool(done.all()):
             break

@@ -255,17 +255,21 @@ def gelu_bwd(g, pre, out):
 
 
 # ----------------------------------------------------------------------------- greedy decode (A12)
-def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale):
-    """One query row per (b, h) over the first Tk cached key rows (include/tw_hip.h)."""
+def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_dev=None, tk_max=None):
+    """One query row per (b, h) over the first Tk (+ *tk_dev) cached key rows (include/tw_hip.h).
+    With tk_dev the host cannot know Tk: tk_max bounds the rows checked for extent."""
     hd = 64
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
         assert t.dtype == torch.bfloat16, nm
+    rows = Tk if tk_dev is None else tk_max
     _need(q, (B - 1) * sqb + H * hd, "decode q")
-    _need(k, (B - 1) * skb + (Tk - 1) * ldk + H * hd, "decode k")
-    _need(v, (B - 1) * svb + (Tk - 1) * ldv + H * hd, "decode v")
+    _need(k, (B - 1) * skb + (rows - 1) * ldk + H * hd, "decode k")
+    _need(v, (B - 1) * svb + (rows - 1) * ldv + H * hd, "decode v")
     _need(o, (B - 1) * sob + H * hd, "decode o")
+    if tk_dev is not None:
+        assert tk_dev.dtype == torch.int32 and tk_max is not None
     call("tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb, o.data_ptr(), sob,
-         B, H, Tk, hd, float(scale), _stream())
+         B, H, Tk, _ptr(tk_dev), hd, float(scale), _stream())
     return o
 
 
@@ -280,14 +284,38 @@ def token_bitmask(ids, V, device):
     return words.to(torch.int32).to(device)
 
 
-def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids):
+def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids,
+                  t_dev=None, begin_col=-1):
     assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
     assert done.dtype == torch.uint8
     _need(logits, (B - 1) * ld + V, "greedy logits")
-    _need(ids, (B - 1) * ids.stride(0) + col + 1, "greedy ids")
+    _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "greedy ids")
     _need(done, B, "greedy done"); _need(next_ids, B, "greedy next")
     for m, nm in ((suppress_bits, "suppress"), (begin_bits, "begin")):
         if m is not None:
             _need(m, (V + 31) // 32, f"greedy {nm} mask")
     call("tw_greedy_select", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
-         int(eos), done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _stream())
+         int(eos), done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev),
+         int(begin_col), _stream())
+
+
+def embed_step(ids, tok, pos, out, t_dev, max_pos):
+    B = ids.numel()
+    D = tok.shape[1]
+    assert ids.dtype == torch.int64 and t_dev.dtype == torch.int32 and out.numel() == B * D
+    assert pos.shape[0] >= max_pos
+    call("tw_embed_step", ids.data_ptr(), tok.data_ptr(), _dt(tok), pos.data_ptr(), _dt(pos), out.data_ptr(),
+         _dt(out), B, D, t_dev.data_ptr(), _stream())
+    return out
+
+
+def kv_append(src, ld_src, cache, ld_row, sb, B, n, t_dev, max_rows):
+    assert src.dtype == torch.bfloat16 and cache.dtype == torch.bfloat16 and t_dev.dtype == torch.int32
+    _need(src, (B - 1) * ld_src + n, "kv_append src")
+    _need(cache, (B - 1) * sb + (max_rows - 1) * ld_row + n, "kv_append cache")
+    call("tw_kv_append", src.data_ptr(), ld_src, cache.data_ptr(), ld_row, sb, B, n, t_dev.data_ptr(), _stream())
+
+
+def step_advance(t_dev, by=1):
+    assert t_dev.dtype == torch.int32 and t_dev.is_cuda
+    call("tw_step_advance", t_dev.data_ptr(), int(by), _stream())

@@ -190,3 +190,15 @@ def test_generate_builds_prompt_and_stops():
         if 50257 in r:
             k = r.index(50257)
             assert all(x == 50257 for x in r[k:])
+
+
+def test_generate_graph_replay_equals_eager():
+    """The HIP-graph replay of the position-independent step emits exactly the eager tokens."""
+    cfg, w, m, GC = _micro()
+    g = load_golden("greedy")
+    m.generation_config = GC(suppress_tokens=g["suppress"].tolist(), begin_suppress_tokens=[220, 50257])
+    prompt = torch.tensor([g["greedy_prompt"].tolist()] * 3)
+    feats = _feats()
+    a = m.generate(feats, decoder_input_ids=prompt, max_length=48, use_graph=True).cpu()
+    b = m.generate(feats, decoder_input_ids=prompt, max_length=48, use_graph=False).cpu()
+    assert torch.equal(a, b)

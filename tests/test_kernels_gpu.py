@@ -133,6 +133,36 @@ def test_gemm_forced_tiles_bit_identical(M, N, K):
             assert torch.equal(outs[name][kind], got), (name, kind)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 16, 8), (5, 1000, 1280), (64, 1281 - 1, 5120), (100, 3840, 1280),
+                                   (128, 200, 64)])
+def test_gemm_skinny_decode_path(M, N, K):
+    """M <= 128 K-major GEMMs (decode steps) take the weight-streaming kernel; every epilogue
+    kind against fp64 (tolerance: one bf16 ulp of the largest value; fp32 out 1e-5 relative)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias, res = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    acc = bf(A).double() @ bf(W).double().T
+    y = bf((acc + bf(bias).double()).float()).float()
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N)
+    assert rel_err(C, acc) < 1e-5
+    Cg, aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV), torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(Ad, Wd, Cg, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, aux=aux, ldaux=N,
+             flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT)
+    gel = bf(torch.nn.functional.gelu(y)).float()
+    assert (aux.float().cpu() - y).abs().max() <= 2 ** -7 * y.abs().max()
+    assert (Cg.float().cpu() - gel).abs().max() <= 2 ** -7 * gel.abs().max() + 1e-6
+    rf = res.clone().to(DEV)                                     # in-place fp32 residual stream
+    ops.gemm(Ad, Wd, rf, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rf, ldr=N, flags=ops.GEMM_ROUND)
+    want = y + res
+    assert (rf.cpu() - want).abs().max() <= 2 ** -7 * y.abs().max() + 1e-5
+    C3 = torch.ones(M, N, device=DEV)
+    ops.gemm(Ad, Wd, C3, M, N, K, lda=K, ldb=K, ldc=N, alpha=0.5, flags=ops.GEMM_ACCUM)
+    assert rel_err(C3 - 1.0, 0.5 * acc) < 1e-5
+
+
 def test_gemm_batched_strided_view():
     """conv2-style zero-copy im2col: A rows = 3 consecutive rows of a padded buffer (lda = 2*C)."""
     from tw import ops
