@@ -742,7 +742,7 @@ __device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float 
 }
 
 template <int MF>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmP p) {
+__global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
   __shared__ float part[4][MF * 16][17];
   const int lane = lane_id(), wave = wave_id_uniform();
   const int n0 = blockIdx.x * 16;
@@ -768,22 +768,36 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmP p) {
     const int k = ks * 32 + 8 * g;
     return (ok && k < p.K) ? *(const bf16x8*)(base + ks * 32) : bf16x8{};
   };
-  int ks = k_beg;
-  for (; ks + 1 < k_end; ks += 2) {                        // two k-steps of loads in flight
-    const bf16x8 w0 = ldk(wp, ks, wok), w1 = ldk(wp, ks + 1, wok);
-    bf16x8 a0[MF], a1[MF];
+  // software pipeline: the fragments of 4 k-steps in flight while the previous 4 compute (the
+  // W bytes come from HBM once; a 2-deep loop left the per-k-step latency exposed)
+  constexpr int D = 4;
+  bf16x8 wb[2][D], ab[2][D][MF];
+  auto load_group = [&](int buf, int k0) {
 #pragma unroll
-    for (int i = 0; i < MF; ++i) { a0[i] = ldk(ap[i], ks, aok[i]); a1[i] = ldk(ap[i], ks + 1, aok[i]); }
+    for (int j = 0; j < D; ++j) {
+      const bool in = k0 + j < k_end;
+      wb[buf][j] = ldk(wp, k0 + j, wok && in);
 #pragma unroll
-    for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, a0[i], acc[i], 0, 0, 0);
+      for (int i = 0; i < MF; ++i) ab[buf][j][i] = ldk(ap[i], k0 + j, aok[i] && in);
+    }
+  };
+  auto mma_group = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < MF; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, a1[i], acc[i], 0, 0, 0);
-  }
-  if (ks < k_end) {
-    const bf16x8 w0 = ldk(wp, ks, wok);
+    for (int j = 0; j < D; ++j)
 #pragma unroll
-    for (int i = 0; i < MF; ++i)
-      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, ldk(ap[i], ks, aok[i]), acc[i], 0, 0, 0);
+      for (int i = 0; i < MF; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[buf][j], ab[buf][j][i], acc[i], 0, 0, 0);
+  };
+  if (k_beg < k_end) {
+    load_group(0, k_beg);
+    int k0 = k_beg;
+    for (; k0 + D < k_end; k0 += 2 * D) {
+      load_group(1, k0 + D);
+      mma_group(0);
+      if (k0 + 2 * D < k_end) load_group(0, k0 + 2 * D);
+      mma_group(1);
+    }
+    if (k0 < k_end) mma_group(0);
   }
   // lane holds C[16i + li][n0 + 4g + r]
 #pragma unroll
@@ -903,7 +917,10 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   if (flags & 2048) tile = 2562;      // 256x256 ping-pong (K-major A and B only)
   const int64_t ntiles = (tile == 256 || tile == 2562) ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
-  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && !(flags & (256 | 512 | 1024 | 2048));
+  // decode-step GEMMs (tools/bench_skinny.py, r01): the weight-streaming kernel wins for N <= 3840
+  // (and N <= 8192 at M <= 64); the LM head and wide M=128 GEMMs stream faster as 128x128 tiles
+  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && (N <= 4096 || (M <= 64 && N <= 8192)) &&
+                      !(flags & (256 | 512 | 1024 | 2048));
   if (skinny && ((uintptr_t)A & 15) == 0) {
     launch_skinny(p, stream);                         // decode-step GEMMs: stream W once
     TW_CHECK_LAUNCH();
