@@ -11,6 +11,13 @@ SuppressTokens (generation_config.suppress_tokens) every step, SuppressTokensAtB
 ([220, eos]) at the first generated step (HF:generation/logits_process.py), argmax,
 stop at eos or max_length.  This oracle recomputes the whole prefix each step (no
 cache) so it shares nothing with the KV-cache path it checks.
+
+Timestamps (`return_timestamps=True`): HF WhisperTimeStampLogitsProcessor (transformers
+logits_process.py; applied after SuppressTokensAtBegin and SuppressTokens, generation_whisper.py
+`_retrieve_logit_processors`) restated in `timestamp_rules`.  Long-form (input longer than 3000
+frames, run_eval.py:659-685 -> HF generate): the sequential window loop of generation_whisper.py
+(`generate` step 6, `_retrieve_segment`, the eos/pad trimming of `generate_with_fallback`) with
+temperature 0 and no fallback thresholds, restated in `longform`.
 """
 from __future__ import annotations
 
@@ -41,3 +48,110 @@ def greedy(model: Ref, feats, prompt, max_length=448, suppress_tokens=(), begin_
         if bool(done.all()):
             break
     return (ids, scores) if return_scores else ids
+
+
+TS_BEGIN, NO_TS = 50364, 50363
+
+
+def timestamp_rules(lg, gen, first, ts_begin=TS_BEGIN, no_ts=NO_TS, eos=50257, max_initial=None):
+    """HF WhisperTimeStampLogitsProcessor on one row.  lg: fp32 [V] scores after the suppress
+    processors, gen: tokens generated so far in this window (after the prompt)."""
+    lg = lg.clone()
+    lg[no_ts] = float("-inf")
+    last_ts = len(gen) >= 1 and gen[-1] >= ts_begin
+    pen_ts = len(gen) < 2 or gen[-2] >= ts_begin
+    if last_ts:
+        if pen_ts:
+            lg[ts_begin:] = float("-inf")
+        else:
+            lg[:eos] = float("-inf")
+    stamps = [t for t in gen if t >= ts_begin]
+    if stamps:
+        lim = stamps[-1] if (last_ts and not pen_ts) else stamps[-1] + 1
+        lg[ts_begin:lim] = float("-inf")
+    if first:
+        lg[:ts_begin] = float("-inf")
+        if max_initial is not None:
+            lg[ts_begin + max_initial + 1:] = float("-inf")
+    lp = torch.log_softmax(lg.float(), -1)
+    if lp[ts_begin:].logsumexp(-1) > lp[:ts_begin].max():
+        lg[:ts_begin] = float("-inf")
+    return lg
+
+
+def greedy_ts(model: Ref, feats, prompt, max_length=448, suppress_tokens=(), begin_suppress=(220, 50257),
+              eos=50257, max_initial=None, enc=None):
+    """Greedy decode of one 3000-frame window with the timestamp rules (no cache)."""
+    enc = model.encoder(feats) if enc is None else enc
+    B = enc.shape[0]
+    ids = torch.tensor(prompt, dtype=torch.long).unsqueeze(0).repeat(B, 1)
+    done = torch.zeros(B, dtype=torch.bool)
+    while ids.shape[1] < max_length:
+        h = model.decoder(ids, enc)
+        lg = model.logits(h[:, -1:])[:, 0].float().clone()
+        if len(suppress_tokens):
+            lg[:, list(suppress_tokens)] = float("-inf")
+        first = ids.shape[1] == len(prompt)
+        if first and len(begin_suppress):
+            lg[:, list(begin_suppress)] = float("-inf")
+        nxt = torch.empty(B, dtype=torch.long)
+        for b in range(B):
+            row = timestamp_rules(lg[b], ids[b, len(prompt):].tolist(), first, eos=eos, max_initial=max_initial)
+            nxt[b] = row.argmax()
+        nxt = torch.where(done, torch.full_like(nxt, eos), nxt)
+        ids = torch.cat([ids, nxt[:, None]], 1)
+        done |= nxt == eos
+        if bool(done.all()):
+            break
+    return ids
+
+
+def retrieve_segment(seq, seek_num_frames, ts_begin=TS_BEGIN, input_stride=2):
+    """HF `_retrieve_segment` (token part): -> (list of token lists, seek offset in frames)."""
+    is_ts = [t >= ts_begin for t in seq]
+    single_end = is_ts[-2:] == [False, True]
+    cut = [i + 1 for i in range(len(seq) - 1) if is_ts[i] and is_ts[i + 1]]
+    if cut:
+        slices = list(cut)
+        if single_end:
+            slices.append(len(seq))
+        else:
+            slices[-1] += 1
+        segs, last = [], 0
+        for c in slices:
+            segs.append(seq[last:c])
+            last = c
+        if single_end:
+            off = seek_num_frames
+        else:
+            off = (seq[last - 2] - ts_begin) * input_stride
+        return segs, off
+    return [list(seq)], seek_num_frames
+
+
+def longform(model: Ref, feats_long, prompt, suppress_tokens=(), begin_suppress=(220, 50257), eos=50257,
+             max_length=448, max_initial=None, window=3000):
+    """HF sequential long-form generate (temperature 0, no thresholds, no prev-token conditioning)
+    for ONE input [80, T]: returns the concatenated segment tokens."""
+    T = feats_long.shape[-1]
+    seek, out = 0, []
+    while seek < T:
+        n = min(window, T - seek)
+        seg = torch.zeros(1, feats_long.shape[0], window, dtype=feats_long.dtype)
+        seg[0, :, :n] = feats_long[:, seek:seek + n]
+        ids = greedy_ts(model, seg, prompt, max_length=max_length, suppress_tokens=suppress_tokens,
+                        begin_suppress=begin_suppress, eos=eos, max_initial=max_initial)
+        seq = ids[0, len(prompt):].tolist()
+        not_final = seek + window < T
+        if not_final and seq and seq[-1] == eos:
+            seq = seq[:-1]
+        if seq and seq[-1] == eos:                 # pad == eos: keep one eos (HF keeps it)
+            k = len(seq)
+            while k > 1 and seq[k - 2] == eos:
+                k -= 1
+            seq = seq[:k]
+        segs, off = retrieve_segment(seq, n)
+        for sgm in segs:
+            out.extend(sgm)
+        seek += off
+    return out

@@ -209,9 +209,46 @@ def gen_greedy(out):
     out["suppress"] = np.array(SUPPRESS)
 
 
+def ts_generation_config():
+    from transformers import GenerationConfig
+    return GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
+                            pad_token_id=SPECIAL["pad"], bos_token_id=SPECIAL["eot"], suppress_tokens=SUPPRESS,
+                            begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=448, num_beams=1,
+                            do_sample=False, no_timestamps_token_id=SPECIAL["notimestamps"], is_multilingual=True,
+                            lang_to_id={"<|en|>": SPECIAL["en"], "<|zh|>": SPECIAL["zh"]},
+                            task_to_id={"transcribe": SPECIAL["transcribe"], "translate": 50358},
+                            max_initial_timestamp_index=50)
+
+
+def longform_features():
+    """Deterministic synthetic log-mel-range features for the long-form fixture (80 x 6500 frames =
+    65 s; feature extraction is pinned separately by mel.npz)."""
+    return (np.random.default_rng(11).standard_normal((1, 80, 6500)) * 0.5).astype(np.float32)
+
+
+def gen_greedy_ts(out):
+    """HF generate(return_timestamps=True): short-form window and a 65 s long-form input."""
+    cfg = CONFIGS["micro"]
+    m = hf_model(cfg, make_weights(cfg, 1, lin_std=0.2)).eval()
+    m.generation_config = ts_generation_config()
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0)]))
+    with torch.no_grad():
+        ids = m.generate(feats, return_timestamps=True, language="zh", task="transcribe", max_new_tokens=48)
+    out["ts_short_ids"] = ids.numpy()
+    lf = torch.from_numpy(longform_features())
+    with torch.no_grad():
+        ids = m.generate(lf, attention_mask=torch.ones(1, lf.shape[-1], dtype=torch.long), return_timestamps=True,
+                         language="zh", task="transcribe")
+    out["ts_long_ids"] = ids.numpy()
+
+
 def main():
     torch.manual_seed(0)
-    for name, fn in (("mel", gen_mel), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy)):
+    only = sys.argv[1:]
+    for name, fn in (("mel", gen_mel), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
+                     ("greedy_ts", gen_greedy_ts)):
+        if only and name not in only:
+            continue
         out = {}
         fn(out)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)

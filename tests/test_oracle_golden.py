@@ -153,3 +153,37 @@ def test_greedy_matches_hf_generate():
     assert n >= 32
     np.testing.assert_array_equal(gen[:, :n], ref[:, :n])
     assert len(set(ref[:, :4].ravel().tolist())) > 3    # fixture is not a degenerate repeat
+
+
+def _ts_setup():
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as mg
+    cfg = CONFIGS["micro"]
+    m = Ref(cfg, to_torch(make_weights(cfg, 1, lin_std=0.2)))
+    prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"]]
+    return mg, m, prompt
+
+
+def test_greedy_timestamps_matches_hf_generate():
+    """Restated WhisperTimeStampLogitsProcessor (oracle/greedy_ref.timestamp_rules) == HF generate(
+    return_timestamps=True), max_initial_timestamp_index 50, suppress + begin-suppress."""
+    g = load_golden("greedy_ts")
+    mg, m, prompt = _ts_setup()
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0)]))
+    with torch.no_grad():
+        ids = greedy_ref.greedy_ts(m, feats, prompt, max_length=len(prompt) + 48, suppress_tokens=mg.SUPPRESS,
+                                   max_initial=50)
+    np.testing.assert_array_equal(ids[:, len(prompt):].numpy(), g["ts_short_ids"])
+    assert (g["ts_short_ids"][:, 0] >= greedy_ref.TS_BEGIN).all()          # first token is a timestamp
+
+
+def test_longform_matches_hf_generate():
+    """Restated sequential long-form loop (seek by last timestamp, segment split, eos trimming) ==
+    HF generate on a 65 s (6500-frame) input."""
+    g = load_golden("greedy_ts")
+    mg, m, prompt = _ts_setup()
+    lf = torch.from_numpy(mg.longform_features())[0]
+    with torch.no_grad():
+        out = greedy_ref.longform(m, lf, prompt, suppress_tokens=mg.SUPPRESS, max_initial=50)
+    assert out == g["ts_long_ids"][0].tolist()
