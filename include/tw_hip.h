@@ -132,6 +132,16 @@ int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64
 int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
                      const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
                      int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col, tw_stream_t stream);
+/* tw_greedy_select_ts: as tw_greedy_select plus HF WhisperTimeStampLogitsProcessor (applied after the
+ * suppress masks): <|notimestamps|> (no_ts) masked, pair / monotonicity rules from the previous two
+ * generated tokens (columns >= begin_col of ids) and last_ts[b] (the row's last emitted timestamp,
+ * -1 = none; updated here), the window's first step limited to timestamps <= ts_begin + max_initial
+ * (max_initial < 0: no limit), and timestamps forced when logsumexp over them exceeds the best text
+ * logit.  col += *t_dev when t_dev != NULL. */
+int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                        const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids, int col,
+                        int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin, int no_ts, int max_initial,
+                        int* last_ts, tw_stream_t stream);
 int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
                   int out_dtype, int B, int D, const int* t_dev, tw_stream_t stream);
 int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n,

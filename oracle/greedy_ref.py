@@ -53,9 +53,11 @@ def greedy(model: Ref, feats, prompt, max_length=448, suppress_tokens=(), begin_
 TS_BEGIN, NO_TS = 50364, 50363
 
 
-def timestamp_rules(lg, gen, first, ts_begin=TS_BEGIN, no_ts=NO_TS, eos=50257, max_initial=None):
+def timestamp_rules(lg, gen, first, ts_begin=TS_BEGIN, no_ts=NO_TS, eos=50257, max_initial=None, apply_mass=True):
     """HF WhisperTimeStampLogitsProcessor on one row.  lg: fp32 [V] scores after the suppress
-    processors, gen: tokens generated so far in this window (after the prompt)."""
+    processors, gen: tokens generated so far in this window (after the prompt).  apply_mass=False
+    skips the final "timestamp probability mass beats every text token" step (tests use it to
+    accept either branch when that comparison is within rounding noise)."""
     lg = lg.clone()
     lg[no_ts] = float("-inf")
     last_ts = len(gen) >= 1 and gen[-1] >= ts_begin
@@ -73,6 +75,8 @@ def timestamp_rules(lg, gen, first, ts_begin=TS_BEGIN, no_ts=NO_TS, eos=50257, m
         lg[:ts_begin] = float("-inf")
         if max_initial is not None:
             lg[ts_begin + max_initial + 1:] = float("-inf")
+    if not apply_mass:
+        return lg
     lp = torch.log_softmax(lg.float(), -1)
     if lp[ts_begin:].logsumexp(-1) > lp[:ts_begin].max():
         lg[:ts_begin] = float("-inf")

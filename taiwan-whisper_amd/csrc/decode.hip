@@ -163,6 +163,94 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
   }
 }
 
+
+// Timestamp decoding (HF WhisperTimeStampLogitsProcessor, applied after the suppress processors):
+// <|notimestamps|> masked; timestamps in pairs (after ts,ts -> text; after text,ts -> ts or eos);
+// timestamps non-decreasing (none below the last one, or below last+1 unless closing a pair);
+// at the window's first step only timestamps <= ts_begin + max_initial; and when the probability
+// mass of all timestamps exceeds the best text token (logsumexp over timestamps > max text logit,
+// the log_softmax shift cancels) only timestamps are eligible.  One pass per row gathers the
+// text argmax, the timestamp argmax and the timestamp logsumexp; last_ts[b] keeps the row's last
+// emitted timestamp (-1: none in this window).
+struct SelTsP {
+  SelP s;
+  int begin_col;              // first generated column of the window
+  int ts_begin, no_ts, max_initial;
+  int* last_ts;
+};
+
+__global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
+  __shared__ float sv[4][3];
+  __shared__ int si[4][2];
+  SelP& p = q.s;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (p.t_dev) p.col += *p.t_dev;
+  const bool first = p.col == q.begin_col;
+  const int64_t* idr = p.ids + b * p.ld_ids;
+  const bool has1 = p.col - 1 >= q.begin_col, has2 = p.col - 2 >= q.begin_col;
+  const bool last_ts = has1 && idr[p.col - 1] >= q.ts_begin;
+  const bool pen_ts = !has2 || idr[p.col - 2] >= q.ts_begin;
+  const int lt = q.last_ts[b];
+  const int lim = lt < 0 ? q.ts_begin : ((last_ts && !pen_ts) ? lt : lt + 1);
+  const int ts_hi = (first && q.max_initial >= 0) ? q.ts_begin + q.max_initial : 0x7fffffff;
+  const bf16* row = p.logits + b * p.ld;
+  float bt = -INFINITY, bs = -INFINITY, se = 0.f;        // best text, best timestamp, sum exp(ts - bs)
+  int it = 0x7fffffff, is = 0x7fffffff;
+  for (int v = tid; v < p.V; v += 256) {
+    float x = bf2f(row[v]);
+    bool m = bit(p.suppress, v) || (first && bit(p.begin, v)) || v == q.no_ts;
+    if (v >= q.ts_begin) {
+      if (last_ts && pen_ts) m = true;
+      if (v < lim || v > ts_hi) m = true;
+      if (!m && x > -INFINITY) {
+        if (x > bs) { se = se * __expf(bs - x) + 1.f; bs = x; is = v; }
+        else { se += __expf(x - bs); if (x == bs && v < is) is = v; }
+      }
+    } else {
+      if ((last_ts && !pen_ts && v < p.eos) || first) m = true;
+      if (!m && (x > bt || (x == bt && v < it))) { bt = x; it = v; }
+    }
+  }
+  // wave reduction: text (max, argmin idx), timestamps (max, argmin idx, rescaled sum)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float obt = __shfl_xor(bt, o, 64), obs = __shfl_xor(bs, o, 64), ose = __shfl_xor(se, o, 64);
+    const int oit = __shfl_xor(it, o, 64), ois = __shfl_xor(is, o, 64);
+    if (obt > bt || (obt == bt && oit < it)) { bt = obt; it = oit; }
+    const float mx = fmaxf(bs, obs);
+    const float ns = (mx == -INFINITY) ? 0.f : se * __expf(bs - mx) + ose * __expf(obs - mx);
+    if (obs > bs || (obs == bs && ois < is)) is = ois;
+    bs = mx;
+    se = ns;
+  }
+  if (lane == 0) { sv[wave][0] = bt; sv[wave][1] = bs; sv[wave][2] = se; si[wave][0] = it; si[wave][1] = is; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) {
+      const float obt = sv[w][0], obs = sv[w][1], ose = sv[w][2];
+      const int oit = si[w][0], ois = si[w][1];
+      if (obt > bt || (obt == bt && oit < it)) { bt = obt; it = oit; }
+      const float mx = fmaxf(bs, obs);
+      const float ns = (mx == -INFINITY) ? 0.f : se * __expf(bs - mx) + ose * __expf(obs - mx);
+      if (obs > bs || (obs == bs && ois < is)) is = ois;
+      bs = mx;
+      se = ns;
+    }
+    int best;
+    const float ts_lse = bs == -INFINITY ? -INFINITY : bs + __logf(se);
+    if (bs > -INFINITY && ts_lse > bt) best = is;                    // timestamp mass wins: text masked
+    else if (bt >= bs && it != 0x7fffffff) best = it;                 // text ids < timestamp ids: ties -> text
+    else if (is != 0x7fffffff) best = is;
+    else best = 0;
+    const bool fin = p.done[b] != 0;
+    const int64_t tok = fin ? p.eos : (int64_t)best;
+    p.ids[b * p.ld_ids + p.col] = tok;
+    p.next[b] = tok;
+    p.done[b] = (fin || tok == p.eos) ? 1 : 0;
+    if (!fin && tok >= q.ts_begin) q.last_ts[b] = (int)tok;
+  }
+}
+
 // x[b] = tok[ids[b]] + pos[*t_dev]   (decoder input embedding of step t, HF modeling_whisper.py:720-735)
 __global__ void embed_step_kernel(const int64_t* __restrict__ ids, const void* __restrict__ tok, int tok_dtype,
                                   const void* __restrict__ pos, int pos_dtype, void* __restrict__ out, int out_dtype,
@@ -191,6 +279,23 @@ __global__ void step_advance_kernel(int* t_dev, int by) {
 }
 
 }  // namespace
+
+extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                                   const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids,
+                                   int col, int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin,
+                                   int no_ts, int max_initial, int* last_ts, hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  if (V <= 0 || ld < V || !done || !ids || !next_ids || !last_ts || ts_begin <= eos || ts_begin > V) return TW_EINVAL;
+  SelTsP q;
+  q.s.logits = (const bf16*)logits; q.s.ld = ld; q.s.V = V;
+  q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
+  q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
+  q.s.t_dev = t_dev; q.s.begin_col = begin_col;
+  q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
+  hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
 
 extern "C" int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype,
                              void* out, int out_dtype, int B, int D, const int* t_dev, hipStream_t stream) {

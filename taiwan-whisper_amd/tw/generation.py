@@ -41,14 +41,9 @@ class DecodeSession:
         d = self.d
         self.self_kv = [torch.empty(B, T_max, 2 * d, dtype=torch.bfloat16, device=dev)
                         for _ in range(cfg.decoder_layers)]
-        self.cross_kv = []
-        for i in range(cfg.decoder_layers):
-            p = f"model.decoder.layers.{i}.encoder_attn"
-            kv = torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=dev)
-            wkv = model.store.span(model.store.p16, p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
-            bkv = model.store.span(model.store.p16, p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
-            model._lin(enc16, wkv, bkv, kv)
-            self.cross_kv.append(kv)
+        self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=dev)
+                         for _ in range(cfg.decoder_layers)]
+        self.set_encoder(enc16)
         self.t_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cur = torch.zeros(B, dtype=torch.int64, device=dev)       # this step's input ids
         self.x = torch.empty(B, d, dtype=model.stream_dtype, device=dev)
@@ -59,6 +54,15 @@ class DecodeSession:
         self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=torch.bfloat16, device=dev)
         self.logits = torch.empty(B, model.Vp, dtype=torch.bfloat16, device=dev)
         self.graph = None
+
+    def set_encoder(self, enc16):
+        """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe)."""
+        m, d = self.m, self.d
+        for i, kv in enumerate(self.cross_kv):
+            p = f"model.decoder.layers.{i}.encoder_attn"
+            wkv = m.store.span(m.store.p16, p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
+            bkv = m.store.span(m.store.p16, p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
+            m._lin(enc16, wkv, bkv, kv)
 
     def _ln(self, x, name):
         m = self.m
@@ -104,9 +108,7 @@ class DecodeSession:
         hN = self._ln(x, "model.decoder.layer_norm")
         m.lm_head(hN, out=self.logits)
         if select is not None:
-            sup, beg, eos, done, ids, P = select
-            F.greedy_select(self.logits, m.Vp, B, m.config.vocab_size, sup, beg, False, eos, done, ids, 1, self.cur,
-                            t_dev=t_dev, begin_col=P)
+            select(self)
         F.step_advance(t_dev)
 
     def capture(self, select):
@@ -146,6 +148,105 @@ def build_prompt(gc, language=None, task=None, return_timestamps=False):
     return ids
 
 
+class _Select:
+    """Per-step token selection into ids[:, t+1] (t read on the device): HF SuppressTokens,
+    SuppressTokensAtBegin and, with timestamps, WhisperTimeStampLogitsProcessor + argmax."""
+
+    def __init__(self, gc, B, V, T_max, P, dev, timestamps):
+        self.V, self.P, self.ts = V, P, timestamps
+        self.eos = int(gc.eos_token_id)
+        self.sup = F.token_bitmask(gc.suppress_tokens or [], V, dev)
+        self.beg = F.token_bitmask(gc.begin_suppress_tokens or [], V, dev)
+        self.ids = torch.full((B, T_max), self.eos, dtype=torch.int64, device=dev)
+        self.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.last_ts = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        self.no_ts = int(gc.no_timestamps_token_id)
+        mi = gc.max_initial_timestamp_index if "max_initial_timestamp_index" in gc else None
+        self.max_initial = -1 if mi is None else int(mi)
+
+    def reset(self, prompt):
+        self.ids.fill_(self.eos)
+        self.ids[:, :self.P] = prompt
+        self.done.zero_()
+        self.last_ts.fill_(-1)
+
+    def __call__(self, sess):
+        B = sess.B
+        if self.ts:
+            F.greedy_select_ts(sess.logits, sess.m.Vp, B, self.V, self.sup, self.beg, self.eos, self.done, self.ids, 1,
+                               sess.cur, self.last_ts, self.P, ts_begin=self.no_ts + 1, no_ts=self.no_ts,
+                               max_initial=self.max_initial, t_dev=sess.t_dev)
+        else:
+            F.greedy_select(sess.logits, sess.m.Vp, B, self.V, self.sup, self.beg, False, self.eos, self.done, self.ids,
+                            1, sess.cur, t_dev=sess.t_dev, begin_col=self.P)
+
+
+class _Decoder:
+    """One greedy decode of B windows with a fixed prompt; reusable across windows (long-form):
+    the captured step graph stays valid because every buffer it touches is reused in place."""
+
+    def __init__(self, model, gc, B, Tk, P, max_length, timestamps, use_graph):
+        self.m, self.P, self.T_max, self.use_graph = model, P, max_length, use_graph
+        self.sess = None
+        self.sel = _Select(gc, B, model.config.vocab_size, max_length, P, model.device, timestamps)
+        self.B, self.Tk = B, Tk
+
+    def run(self, enc16, prompt):
+        """prompt: int64 [B, P] (device) -> generated ids [B, L] (device), HF trimming."""
+        sel, P = self.sel, self.P
+        if self.sess is None:
+            self.sess = DecodeSession(self.m, enc16, self.B, self.Tk, self.T_max)
+        else:
+            self.sess.set_encoder(enc16)
+        sess = self.sess
+        sel.reset(prompt)
+        sess.t_dev.zero_()
+        for t in range(P - 1):                                   # prefill the cache with the prompt
+            sess.cur.copy_(sel.ids[:, t])
+            sess.step()
+        sess.cur.copy_(sel.ids[:, P - 1])
+        if self.use_graph and sess.graph is None:
+            sess.capture(sel)
+        t = P - 1
+        while t + 1 < self.T_max:
+            if self.use_graph:
+                sess.graph.replay()
+            else:
+                sess.step(sel)
+            t += 1
+            if (t - P) % 8 == 7 and bool(sel.done.all()):
+                break
+        gen = sel.ids[:, P:t + 1]
+        # trim trailing columns in which every row had already finished (HF stops at the step
+        # where the last row emits eos)
+        is_eos = (gen == sel.eos).cpu()
+        B = gen.shape[0]
+        first = torch.where(is_eos.any(1), is_eos.int().argmax(1), torch.full((B,), gen.shape[1]))
+        L = int(min(gen.shape[1], int(first.max()) + 1)) if B else 0
+        return gen[:, :L]
+
+
+def retrieve_segment(seq, seek_num_frames, ts_begin=50364, input_stride=2):
+    """HF `_retrieve_segment` (generation_whisper.py), token part: split a window's tokens at
+    consecutive timestamp pairs -> (segments, seek offset in feature frames)."""
+    is_ts = [t >= ts_begin for t in seq]
+    single_end = is_ts[-2:] == [False, True]
+    cut = [i + 1 for i in range(len(seq) - 1) if is_ts[i] and is_ts[i + 1]]
+    if not cut:
+        return [list(seq)], seek_num_frames
+    slices = list(cut)
+    if single_end:
+        slices.append(len(seq))
+    else:
+        slices[-1] += 1
+    segs, last = [], 0
+    for c in slices:
+        segs.append(list(seq[last:c]))
+        last = c
+    off = seek_num_frames if single_end else (seq[last - 2] - ts_begin) * input_stride
+    return segs, off
+
+
 @torch.no_grad()
 def generate(model, input_features=None, max_length=None, num_beams=1, return_timestamps=False, language=None,
              task=None, decoder_input_ids=None, max_new_tokens=None, encoder_outputs=None, attention_mask=None,
@@ -153,14 +254,19 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     from .config import GenerationConfig
     if num_beams not in (None, 1):
         raise NotImplementedError("tw generate: greedy only (num_beams=1, as every reference call site)")
-    if kw.get("do_sample"):
-        raise NotImplementedError("tw generate: sampling is not on the hot path")
-    if return_timestamps:
-        raise NotImplementedError("tw generate: timestamp decoding is SURVEY.md §8f item 3 (long-form), not built")
+    if kw.get("do_sample") or kw.get("temperature") not in (None, 0, 0.0):
+        raise NotImplementedError("tw generate: sampling / temperature fallback is not built (greedy only)")
     gc = model.generation_config if model.generation_config is not None else GenerationConfig()
     if not isinstance(gc, GenerationConfig):
         gc = GenerationConfig(gc)
+    if gc.eos_token_id is None:
+        gc.eos_token_id = model.config.eos_token_id
     cfg = model.config
+    use_graph = True if use_graph is None else use_graph
+    window = 2 * cfg.max_source_positions                     # 3000 feature frames = 30 s
+    if encoder_outputs is None and input_features is not None and input_features.shape[-1] > window:
+        return _longform(model, gc, input_features, attention_mask, language, task, max_length, max_new_tokens,
+                         use_graph, window, kw.get("_trace"))
     if encoder_outputs is not None:
         enc = encoder_outputs.last_hidden_state if hasattr(encoder_outputs, "last_hidden_state") else encoder_outputs[0]
         B, Tk = enc.shape[0], enc.shape[1]
@@ -184,36 +290,60 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     max_length = min(int(max_length), cfg.max_target_positions)
     if P >= max_length:
         return torch.empty(B, 0, dtype=torch.int64, device=model.device)
+    dec = _Decoder(model, gc, B, Tk, P, max_length, bool(return_timestamps), use_graph)
+    return dec.run(enc16, prompt.to(model.device))
+
+
+def _longform(model, gc, feats, attention_mask, language, task, max_length, max_new_tokens, use_graph, window,
+              trace=None):
+    """HF sequential long-form generate (generation_whisper.py step 6; temperature 0, no fallback
+    thresholds, no previous-text conditioning): per input, 30 s windows from `seek`, greedy with
+    timestamp rules, trailing eos/pad trimmed, segments split at consecutive timestamps, seek
+    advanced by the last timestamp (or the whole window on a single-timestamp ending); returns
+    the concatenated segment tokens, right-padded with pad."""
+    cfg = model.config
     dev = model.device
-    eos = int(gc.eos_token_id if gc.eos_token_id is not None else cfg.eos_token_id)
-    V = cfg.vocab_size
-    ids = torch.full((B, max_length), eos, dtype=torch.int64, device=dev)
-    ids[:, :P] = prompt.to(dev)
-    done = torch.zeros(B, dtype=torch.uint8, device=dev)
-    sup = F.token_bitmask(gc.suppress_tokens or [], V, dev)
-    beg = F.token_bitmask(gc.begin_suppress_tokens or [], V, dev)
-    sess = DecodeSession(model, enc16, B, Tk, max_length)
-    for t in range(P - 1):                                   # prefill the cache with the prompt
-        sess.cur.copy_(ids[:, t])
-        sess.step()
-    sess.cur.copy_(ids[:, P - 1])
-    select = (sup, beg, eos, done, ids, P)
-    graph = use_graph if use_graph is not None else True
-    if graph:
-        sess.capture(select)
-    t = P - 1
-    while t + 1 < max_length:
-        if graph:
-            sess.graph.replay()
-        else:
-            sess.step(select)
-        t += 1
-        if (t - P) % 8 == 7 and bool(done.all()):
-            break
-    gen = ids[:, P:t + 1]
-    # trim trailing columns in which every row had already finished (HF stops at the step
-    # where the last row emits eos)
-    is_eos = (gen == eos).cpu()
-    first = torch.where(is_eos.any(1), is_eos.int().argmax(1), torch.full((B,), gen.shape[1]))
-    L = int(min(gen.shape[1], int(first.max()) + 1)) if B else 0
-    return gen[:, :L]
+    feats = feats.to(dev, torch.float32)
+    B, nmel, T = feats.shape
+    lens = attention_mask.sum(-1).tolist() if attention_mask is not None else [T] * B
+    prompt = torch.tensor(build_prompt(gc, language, task, True), dtype=torch.int64, device=dev)[None]
+    P = prompt.shape[1]
+    if max_new_tokens is not None:
+        max_length = P + int(max_new_tokens)
+    max_length = min(int(max_length or gc.max_length or cfg.max_target_positions), cfg.max_target_positions)
+    eos, pad = int(gc.eos_token_id), int(gc.pad_token_id if gc.pad_token_id is not None else gc.eos_token_id)
+    ts_begin = int(gc.no_timestamps_token_id) + 1
+    dec = _Decoder(model, gc, 1, cfg.max_source_positions, P, max_length, True, use_graph)
+    seg_in = torch.zeros(1, nmel, window, dtype=torch.float32, device=dev)
+    outs = []
+    for b in range(B):
+        Tb = int(lens[b])
+        seek, out = 0, []
+        while seek < Tb:
+            n = min(window, Tb - seek)
+            seg_in.zero_()
+            seg_in[0, :, :n] = feats[b, :, seek:seek + n]
+            enc16 = model.encode(model.conv_input(seg_in))
+            seq = dec.run(enc16, prompt)[0].tolist()
+            if trace is not None:
+                trace.append(dict(b=b, seek=seek, n=n, raw=list(seq)))
+            if seek + window < Tb and seq and seq[-1] == eos:   # not the last window: cut a predicted eos
+                seq = seq[:-1]
+            if seq and seq[-1] == pad:                          # trailing pads (pad == eos keeps one)
+                k = len(seq)
+                while k > 1 and seq[k - 2] == pad:
+                    k -= 1
+                seq = seq[:k] if pad == eos else seq[:k - 1]
+            if not seq:
+                seek += n
+                continue
+            segs, off = retrieve_segment(seq, n, ts_begin)
+            for sgm in segs:
+                out.extend(sgm)
+            seek += off if off > 0 else n          # a closing <|0.00|> pair would not advance: take the window
+        outs.append(out)
+    L = max((len(o) for o in outs), default=0)
+    res = torch.full((B, L), pad, dtype=torch.int64)
+    for b, o in enumerate(outs):
+        res[b, :len(o)] = torch.tensor(o, dtype=torch.int64)
+    return res.to(dev)

@@ -299,6 +299,22 @@ def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos,
          int(begin_col), _stream())
 
 
+def greedy_select_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids, col, next_ids, last_ts,
+                     begin_col, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
+    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
+    assert done.dtype == torch.uint8 and last_ts.dtype == torch.int32
+    _need(logits, (B - 1) * ld + V, "greedy logits")
+    _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "greedy ids")
+    _need(done, B, "greedy done"); _need(next_ids, B, "greedy next"); _need(last_ts, B, "greedy last_ts")
+    for m, nm in ((suppress_bits, "suppress"), (begin_bits, "begin")):
+        if m is not None:
+            _need(m, (V + 31) // 32, f"greedy {nm} mask")
+    call("tw_greedy_select_ts", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(eos),
+         done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev), int(begin_col),
+         int(ts_begin), int(no_ts), int(max_initial if max_initial is not None else -1), last_ts.data_ptr(),
+         _stream())
+
+
 def embed_step(ids, tok, pos, out, t_dev, max_pos):
     B = ids.numel()
     D = tok.shape[1]

@@ -202,3 +202,159 @@ def test_generate_graph_replay_equals_eager():
     a = m.generate(feats, decoder_input_ids=prompt, max_length=48, use_graph=True).cpu()
     b = m.generate(feats, decoder_input_ids=prompt, max_length=48, use_graph=False).cpu()
     assert torch.equal(a, b)
+
+
+def _ts_model():
+    import os, sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as mg
+    cfg, w, m, GC = _micro()
+    gc = mg.ts_generation_config().to_dict()
+    m.generation_config = GC({k: gc[k] for k in ("decoder_start_token_id", "eos_token_id", "pad_token_id",
+                                                  "suppress_tokens", "begin_suppress_tokens", "max_length",
+                                                  "no_timestamps_token_id", "is_multilingual", "lang_to_id",
+                                                  "task_to_id", "max_initial_timestamp_index")})
+    return mg, cfg, w, m
+
+
+def test_generate_timestamps_short_form():
+    """return_timestamps=True on one window: every emitted token obeys the HF timestamp rules
+    (restated in the oracle) against the bf16-autocast oracle teacher-forced along our tokens
+    (argmax within MARGIN; when the timestamp-mass decision itself is within MARGIN either
+    branch is accepted); exact agreement with the HF fp32 fixture for >= 8 tokens."""
+    from oracle import greedy_ref
+    from oracle.whisper_ref import Ref, to_torch
+    mg, cfg, w, m = _ts_model()
+    g = load_golden("greedy_ts")
+    feats = torch.from_numpy(np.stack([_feats()[0].numpy(), _feats()[1].numpy()]))
+    gen = m.generate(feats, return_timestamps=True, language="zh", task="transcribe", max_new_tokens=48).cpu()
+    prompt = [50258, 50260, 50359]
+    P = len(prompt)
+    seq = torch.cat([torch.tensor([prompt] * 2), gen], 1)
+    ref = Ref(cfg, to_torch(w), amp=True)
+    with torch.no_grad():
+        lg = ref.logits(ref.decoder(seq[:, :-1], ref.encoder(feats))).float()
+    sup = mg.SUPPRESS
+    for b in range(2):
+        for j in range(gen.shape[1]):
+            if j > 0 and int(gen[b, j - 1]) == 50257:
+                break
+            row = lg[b, P - 1 + j].clone()
+            row[sup] = -float("inf")
+            if j == 0:
+                row[[220, 50257]] = -float("inf")
+            hist = gen[b, :j].tolist()
+            tok = int(gen[b, j])
+            full = greedy_ref.timestamp_rules(row, hist, j == 0, max_initial=50)
+            tol = max(MARGIN, 2 ** -7 * float(full.max().abs()))      # 2 bf16 ulps of the logit
+            ok = float(full.max() - full[tok]) <= tol
+            if not ok:          # the timestamp-mass comparison within noise: accept the other branch
+                pre = greedy_ref.timestamp_rules(row, hist, j == 0, max_initial=50, apply_mass=False)
+                ts_lse = float(pre[50364:].logsumexp(-1))
+                near = abs(ts_lse - float(pre[:50364].max())) <= tol
+                ok = near and float(pre.max() - pre[tok]) <= tol
+            assert ok, (b, j, tok, float(full.max()), float(full[tok]))
+    # HF fp32 fixture: identical up to the first divergence, which must be an fp32 near-tie of the
+    # rule-processed row (fp32 oracle teacher-forced along the common prefix)
+    hf = g["ts_short_ids"]
+    ref32 = Ref(cfg, to_torch(w))
+    with torch.no_grad():
+        lg32 = ref32.logits(ref32.decoder(seq[:, :-1], ref32.encoder(feats))).float()
+    for b in range(2):
+        n = min(hf.shape[1], gen.shape[1])
+        k = next((i for i in range(n) if int(gen[b, i]) != int(hf[b, i])), n)
+        if k < n:
+            row = lg32[b, P - 1 + k].clone()
+            row[sup] = -float("inf")
+            if k == 0:
+                row[[220, 50257]] = -float("inf")
+            pre = greedy_ref.timestamp_rules(row, gen[b, :k].tolist(), k == 0, max_initial=50, apply_mass=False)
+            a, h = float(pre[int(gen[b, k])]), float(pre[int(hf[b, k])])
+            scale = float(lg32[b, P - 1 + k].abs().max())
+            assert abs(a - h) <= 0.02 * scale, (b, k, a, h, scale)
+    assert (gen[:, 0] >= 50364).all()
+
+
+def _check_ts_window(ref, feats1, prompt, toks, sup, b=0):
+    """bf16-autocast oracle teacher-forced along one window's tokens: each token obeys the HF
+    timestamp rules (argmax within 2 bf16 ulps; either branch when the mass rule is a tie)."""
+    from oracle import greedy_ref
+    P = len(prompt)
+    seq = torch.tensor([prompt + toks])
+    with torch.no_grad():
+        lg = ref.logits(ref.decoder(seq[:, :-1], ref.encoder(feats1))).float()[0]
+    for j, tok in enumerate(toks):
+        if j > 0 and toks[j - 1] == 50257:
+            break
+        row = lg[P - 1 + j].clone()
+        row[sup] = -float("inf")
+        if j == 0:
+            row[[220, 50257]] = -float("inf")
+        full = greedy_ref.timestamp_rules(row, toks[:j], j == 0, max_initial=50)
+        # up to 4 bf16 ulps: hundreds of cached positions accumulate in a different order
+        tol = max(MARGIN, 2 ** -6 * float(full.max().abs()))
+        ok = float(full.max() - full[tok]) <= tol
+        if not ok:
+            pre = greedy_ref.timestamp_rules(row, toks[:j], j == 0, max_initial=50, apply_mass=False)
+            near = abs(float(pre[50364:].logsumexp(-1)) - float(pre[:50364].max())) <= tol
+            ok = near and float(pre.max() - pre[tok]) <= tol
+        assert ok, (j, tok, float(full.max()), float(full[tok]))
+
+
+def test_generate_longform_matches_hf():
+    """65 s input (6500 frames), sequential 30 s windows.  (1) every window's decode obeys the
+    timestamp rules vs the bf16-autocast oracle; (2) the host loop (eos/pad trimming, segment split,
+    seek by last timestamp) applied to those window outputs is the oracle's restatement of HF's
+    loop; (3) vs the HF fp32 fixture: identical up to the first divergence, which is an fp32
+    near-tie inside the first window."""
+    from oracle import greedy_ref
+    from oracle.whisper_ref import Ref, to_torch
+    mg, cfg, w, m = _ts_model()
+    g = load_golden("greedy_ts")
+    lf = torch.from_numpy(mg.longform_features())
+    trace = []
+    out = m.generate(lf, attention_mask=torch.ones(1, lf.shape[-1], dtype=torch.long), return_timestamps=True,
+                     language="zh", task="transcribe", _trace=trace).cpu()[0].tolist()
+    prompt = [50258, 50260, 50359]
+    ref = Ref(cfg, to_torch(w), amp=True)
+    T = lf.shape[-1]
+    seek, rebuilt = 0, []
+    for tr in trace:
+        assert tr["seek"] == seek
+        n = min(3000, T - seek)
+        seg = torch.zeros(1, 80, 3000)
+        seg[0, :, :n] = lf[0, :, seek:seek + n]
+        _check_ts_window(ref, seg, prompt, tr["raw"], mg.SUPPRESS)
+        seq = list(tr["raw"])
+        if seek + 3000 < T and seq and seq[-1] == 50257:
+            seq = seq[:-1]
+        segs, off = greedy_ref.retrieve_segment(seq, n)
+        for sgm in segs:
+            rebuilt.extend(sgm)
+        seek += off if off > 0 else n
+    assert seek >= T and rebuilt == out and len(trace) >= 3
+    hf = g["ts_long_ids"][0].tolist()
+    if out == hf:
+        return
+    # HF's output starts with its window-0 segments, a prefix of its window-0 raw tokens: the first
+    # raw token of our window 0 that differs from HF's output is where bf16 and fp32 parted; it
+    # must be an fp32 near-tie of the rule-processed row
+    first = trace[0]["raw"]
+    k = next((i for i in range(min(len(first), len(hf))) if first[i] != hf[i]), None)
+    assert k is not None and k >= 8, (k, first[:40], hf[:40])
+    ref32 = Ref(cfg, to_torch(w))
+    seg = torch.zeros(1, 80, 3000)
+    seg[0] = lf[0, :, :3000]
+    seq = torch.tensor([prompt + first[:k + 1]])
+    with torch.no_grad():
+        row = ref32.logits(ref32.decoder(seq[:, :-1], ref32.encoder(seg))).float()[0, -1].clone()
+    row[mg.SUPPRESS] = -float("inf")
+    pre = greedy_ref.timestamp_rules(row, first[:k], k == 0, max_initial=50, apply_mass=False)
+    scale = float(row[torch.isfinite(row)].abs().max())
+    token_tie = abs(float(pre[first[k]]) - float(pre[hf[k]])) <= 0.02 * scale
+    # or the "timestamp mass beats the best text token" decision is the near-tie: each side took
+    # the argmax of its branch
+    ts_lse, max_text = float(pre[50364:].logsumexp(-1)), float(pre[:50364].max())
+    mass_tie = (abs(ts_lse - max_text) <= 0.02 * scale
+                and {first[k], hf[k]} == {int(pre[:50364].argmax()), 50364 + int(pre[50364:].argmax())})
+    assert token_tie or mass_tie, (k, first[k], hf[k], ts_lse, max_text)
