@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--clips", type=int, default=128)
     ap.add_argument("--config", default="large-v2")
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--longform-seconds", type=float, default=0.0,
+                    help="config c5: one input of this many seconds, return_timestamps, --new-tokens per window")
     a = ap.parse_args()
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
     from oracle.weights import CONFIGS
@@ -30,6 +32,23 @@ def main():
     random_init_(m, seed=0)
     m.generation_config = GenerationConfig(suppress_tokens=[50257], begin_suppress_tokens=[220, 50257],
                                            lang_to_id={"<|zh|>": 50260})
+    if a.longform_seconds > 0:
+        T = int(a.longform_seconds * 100)
+        lf = torch.randn(1, 80, T, device="cuda") * 0.3
+        trace = []
+        m.generate(lf[:, :, :3500], return_timestamps=True, language="zh", task="transcribe", max_new_tokens=8,
+                   use_graph=not a.eager)                                                     # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = m.generate(lf, return_timestamps=True, language="zh", task="transcribe", max_new_tokens=a.new_tokens,
+                         use_graph=not a.eager, _trace=trace)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        steps = sum(len(t["raw"]) for t in trace)
+        print(f"c5 long-form {a.config}: {a.longform_seconds:.0f} s audio, {len(trace)} windows, {steps} decode steps, "
+              f"{out.shape[1]} output tokens: {dt:.2f} s wall ({a.longform_seconds / dt:.1f}x real time, "
+              f"{dt / max(steps, 1) * 1e3:.2f} ms/step at batch 1)", flush=True)
+        return
     feats = torch.randn(a.batch, 80, 3000, device="cuda") * 0.3
     m.generate(feats[:2], language="zh", task="transcribe", max_new_tokens=4, use_graph=not a.eager)   # warm-up
     torch.cuda.synchronize()
