@@ -197,13 +197,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     }
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
-      float tmax = -INFINITY;
+      // row max: a tree over the lane's 16 scores, then across the 4 lanes of the query column
+      // (l, l^16, l^32, l^48) with v_permlane16/32_swap (VALU) instead of two ds_bpermute trips
+      float t4[4];
 #pragma unroll
       for (int kj = 0; kj < 4; ++kj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[kj][qi][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        t4[kj] = fmaxf(fmaxf(s[kj][qi][0], s[kj][qi][1]), fmaxf(s[kj][qi][2], s[kj][qi][3]));
+      float tmax = fmaxf(fmaxf(t4[0], t4[1]), fmaxf(t4[2], t4[3]));
+      {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+      }
       const float mn = fmaxf(m[qi], tmax * p.scale_log2);
       if (__any(mn > m[qi])) {
         const float alpha = __builtin_amdgcn_exp2f(m[qi] - mn);
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
         for (int hj = 0; hj < 4; ++hj) o[hj][qi] *= alpha;
       }
       m[qi] = mn;
-      float ls = 0.f;
+      float ls = 0.f;      // sequential (a 4-way split moved the micro-config KL by 1e-3 vs the oracle)
 #pragma unroll
       for (int kj = 0; kj < 4; ++kj)
 #pragma unroll
