@@ -12,6 +12,7 @@ Everything runs on the GPU through libtw_hip.so; nothing on the step synchronise
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -62,6 +63,7 @@ class DistillationTrainer:
         if freeze_embed_positions:
             student.set_trainable("model.decoder.embed_positions", False)
         self.train_encoder = not freeze_encoder
+        self.freeze_encoder, self.freeze_decoder = freeze_encoder, freeze_decoder
         self.share = freeze_encoder and student.config.d_model == teacher.config.d_model
         student.pack_for_training()
         student.sync_bf16()
@@ -208,3 +210,95 @@ class DistillationTrainer:
         self.step = int(st["step"])
         self.m_buf.copy_(st["exp_avg"])
         self.v_buf.copy_(st["exp_avg_sq"])
+
+    def _moment_view(self, buf, n):
+        """HF-shaped view of a trainable segment of a flat moment buffer (engine layout)."""
+        from .modeling import to_hf
+        s = self.s
+        o = s.store.offset[n]
+        return to_hf(n, buf[o: o + s.store.numel(n)].view(s.store.segs[n]), s.config)
+
+    def optimizer_state_dict(self):
+        """torch.optim.AdamW.state_dict() of the reference's optimizer (tw/checkpoint.py groups)."""
+        from .checkpoint import optimizer_groups
+        g0, g1 = optimizer_groups(self.s.config, self.freeze_encoder, self.freeze_decoder)
+        state, idx = {}, 0
+        groups = []
+        lr = self.lr_at(self.step)
+        for names, wd in ((g0, self.wd), (g1, 0.0)):
+            ids = []
+            for n in names:
+                if n in self.s.trainable and self.step > 0:
+                    state[idx] = {"step": torch.tensor(float(self.step)),
+                                  "exp_avg": self._moment_view(self.m_buf, n).detach().cpu().clone(),
+                                  "exp_avg_sq": self._moment_view(self.v_buf, n).detach().cpu().clone()}
+                ids.append(idx)
+                idx += 1
+            groups.append({"lr": lr, "betas": (self.b1, self.b2), "eps": self.eps, "weight_decay": wd,
+                           "amsgrad": False, "foreach": None, "maximize": False, "capturable": False,
+                           "differentiable": False, "fused": None, "decoupled_weight_decay": True,
+                           "initial_lr": self.lr, "params": ids})
+        return {"state": state, "param_groups": groups}
+
+    def load_optimizer_state_dict(self, sd):
+        """Inverse of optimizer_state_dict (also accepts the reference's own optimizer.bin)."""
+        from .checkpoint import optimizer_groups
+        g0, g1 = optimizer_groups(self.s.config, self.freeze_encoder, self.freeze_decoder)
+        order = g0 + g1
+        if len(order) != sum(len(g["params"]) for g in sd["param_groups"]):
+            raise ValueError("optimizer state: parameter count differs from the reference grouping")
+        flat = [i for g in sd["param_groups"] for i in g["params"]]
+        steps = set()
+        self.m_buf.zero_()
+        self.v_buf.zero_()
+        for n, i in zip(order, flat):
+            st = sd["state"].get(i)
+            if st is None:
+                continue
+            if n not in self.s.trainable:
+                raise ValueError(f"optimizer state for {n}, which is frozen here")
+            self._moment_view(self.m_buf, n).copy_(st["exp_avg"])
+            self._moment_view(self.v_buf, n).copy_(st["exp_avg_sq"])
+            steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"optimizer state: mixed step counts {sorted(steps)}")
+        self.step = steps.pop() if steps else 0
+
+    def scheduler_state_dict(self):
+        """LambdaLR.state_dict() of get_scheduler(...) stepped world times per update (:1458-1463)."""
+        n = self.step * self.world
+        return {"base_lrs": [self.lr, self.lr], "last_epoch": n, "verbose": False, "_step_count": n + 1,
+                "_get_lr_called_within_step": False, "_last_lr": [self.lr_at(self.step)] * 2,
+                "lr_lambdas": [None, None]}
+
+    def save_state(self, output_dir, save_teacher=True, rank=0):
+        """accelerator.save_state layout (tw/checkpoint.py)."""
+        from safetensors.torch import save_file
+        os.makedirs(output_dir, exist_ok=True)
+        if rank == 0:
+            for i, m in enumerate([self.s] + ([self.t] if save_teacher else [])):
+                sd = {k: v.detach().to("cpu").contiguous() for k, v in m.state_dict().items() if k != "proj_out.weight"}
+                save_file(sd, os.path.join(output_dir, "model.safetensors" if i == 0 else f"model_{i}.safetensors"),
+                          metadata={"format": "pt"})
+            torch.save(self.optimizer_state_dict(), os.path.join(output_dir, "optimizer.bin"))
+            torch.save(self.scheduler_state_dict(), os.path.join(output_dir, "scheduler.bin"))
+        torch.save({"torch_manual_seed": torch.get_rng_state(), "step": self.step},
+                   os.path.join(output_dir, f"random_states_{rank}.pkl"))
+
+    def load_state(self, input_dir):
+        """accelerator.load_state(dir) equivalent: student weights, optimizer moments and step.
+        Files are read with safe loaders only (safetensors; torch.load(weights_only=True))."""
+        from safetensors.torch import load_file
+        sd = load_file(os.path.join(input_dir, "model.safetensors"))
+        sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+        self.s.load_state_dict(sd, strict=False)
+        self.s.sync_bf16()
+        opt = torch.load(os.path.join(input_dir, "optimizer.bin"), map_location="cpu", weights_only=True)
+        self.load_optimizer_state_dict(opt)
+        sp = os.path.join(input_dir, "scheduler.bin")
+        if os.path.exists(sp):
+            sch = torch.load(sp, map_location="cpu", weights_only=True)
+            if int(sch["last_epoch"]) != self.step * self.world:
+                raise ValueError(f"scheduler last_epoch {sch['last_epoch']} != step {self.step} x world {self.world}")
+        self.micro = 0
+        self.s.grad.zero_()

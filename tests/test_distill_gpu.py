@@ -9,6 +9,8 @@ reference's train_step under CUDA bf16 autocast with the same rounding points as
     order, so individual bf16 elements may differ by one ulp);
   * AdamW-updated parameters: <= 2e-3 relative L2 of the update.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -125,3 +127,83 @@ def test_train_step_matches_oracle(freeze_encoder):
         agree = (torch.sign(got) == torch.sign(want)).float().mean().item()
         assert agree > 0.995, (n, agree)
         assert (got[stable] - want[stable]).norm() / want[stable].norm() < 2e-3, n
+
+
+def test_checkpoint_resume_and_reference_optimizer_interop(tmp_path):
+    """save_state / load_state in accelerate's layout (tw/checkpoint.py):
+    (1) resume == uninterrupted training (same kernels, same inputs);
+    (2) optimizer.bin loads into the reference's torch AdamW over HF named_parameters() groups and
+        the per-parameter moments equal ours; a torch-written optimizer.bin loads back into ours."""
+    import transformers
+    from safetensors.torch import load_file
+    from oracle import distill_ref
+    from oracle.weights import CONFIGS
+    from tw.distill import DistillationTrainer
+    g, feats, dec, lab = _batch()
+    batch = dict(input_features=feats.cuda(), decoder_input_ids=dec.cuda(), labels=lab.cuda())
+    kw = dict(learning_rate=1e-3, warmup_steps=3, weight_decay=0.01, freeze_encoder=True)
+    _, _, _, s, t = _models(True)
+    a = DistillationTrainer(s, t, **kw)
+    a.train_step(batch)
+    a.train_step(batch)
+    ck = tmp_path / "checkpoint-2-epoch-0"
+    a.save_state(str(ck))
+    assert sorted(os.listdir(ck)) == ["model.safetensors", "model_1.safetensors", "optimizer.bin",
+                                      "random_states_0.pkl", "scheduler.bin"]
+    a.train_step(batch)
+    torch.cuda.synchronize()
+    # (1) fresh student with different weights, resumed from the checkpoint
+    _, _, _, s2, t2 = _models(True)
+    with torch.no_grad():
+        s2.store.p32.mul_(0.5)
+    b = DistillationTrainer(s2, t2, **kw)
+    b.load_state(str(ck))
+    assert b.step == 2
+    b.train_step(batch)
+    torch.cuda.synchronize()
+    for n in sorted(s.trainable):
+        x, y = s.state_view(n).float(), s2.state_view(n).float()
+        assert torch.allclose(x, y, rtol=1e-6, atol=1e-7), n
+    # (2) the reference's optimizer over an HF model built from model.safetensors
+    cfg = CONFIGS["micro"]
+    hf = transformers.WhisperForConditionalGeneration(transformers.WhisperConfig(**cfg))
+    missing, unexpected = hf.load_state_dict(load_file(str(ck / "model.safetensors")), strict=False)
+    assert missing == ["proj_out.weight"] and unexpected == []
+    for n, p in hf.named_parameters():
+        p.requires_grad_(n in s.trainable)
+    names = [n for n, _ in hf.named_parameters()]
+    decay = set(distill_ref.decay_parameter_names(names, ("model.encoder.",)))
+    opt = torch.optim.AdamW([dict(params=[p for n, p in hf.named_parameters() if n in decay], weight_decay=0.01),
+                             dict(params=[p for n, p in hf.named_parameters() if n not in decay], weight_decay=0.0)],
+                            lr=1e-3)
+    opt.load_state_dict(torch.load(str(ck / "optimizer.bin"), weights_only=True))
+    byname = dict(hf.named_parameters())
+    from tw.modeling import to_hf
+    for n in names:
+        st = opt.state.get(byname[n], {})
+        assert bool(st) == (n in s.trainable), n
+        if st:
+            assert float(st["step"]) == 2.0
+    # moments as of step 2 (trainer b resumed from them before stepping): check against a 3rd load
+    c = DistillationTrainer(*_models(True)[3:], **kw)
+    c.load_state(str(ck))
+    for n in names:
+        st = opt.state.get(byname[n])
+        if st:
+            o = c.s.store.offset[n]
+            m = to_hf(n, c.m_buf[o: o + c.s.store.numel(n)].view(c.s.store.segs[n]), c.s.config)
+            assert torch.equal(st["exp_avg"], m.cpu()), n
+    # torch -> ours: perturb the reference optimizer's moments, save, load, compare
+    for st in opt.state.values():
+        st["exp_avg"].mul_(-3.0)
+        st["exp_avg_sq"].mul_(2.0)
+    torch.save(opt.state_dict(), str(ck / "optimizer.bin"))
+    c.load_state(str(ck))
+    for n in names:
+        st = opt.state.get(byname[n])
+        if st:
+            o = c.s.store.offset[n]
+            v = to_hf(n, c.v_buf[o: o + c.s.store.numel(n)].view(c.s.store.segs[n]), c.s.config)
+            assert torch.equal(st["exp_avg_sq"], v.cpu()), n
+    sch = torch.load(str(ck / "scheduler.bin"), weights_only=True)
+    assert sch["last_epoch"] == 2
