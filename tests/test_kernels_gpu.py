@@ -133,6 +133,47 @@ def test_gemm_forced_tiles_bit_identical(M, N, K):
             assert torch.equal(outs[name][kind], got), (name, kind)
 
 
+@pytest.mark.parametrize("M,N,K", [(8200, 2056, 320), (8200, 2056, 128), (4104, 4096, 1344), (520, 264, 64)])
+def test_gemm_pp_persistent_ragged(M, N, K):
+    """Persistent ping-pong kernel with more tiles than workgroups (the K-tile stream runs across
+    tiles, the next tile's first K-tiles in flight during the epilogue; at K <= 128 every
+    iteration is a tile's last), ragged M and N (masked rows/columns), odd K-tile counts.  Every fast kind (bias+round bf16, bias+round+GELU, in-place bf16 residual) must equal
+    the 128x128 kernel bit for bit (same K order) and the fp64 reference within one bf16 ulp."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias, res = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    acc = bf(A).double() @ bf(W).double().T
+    y = bf((acc + bf(bias).double()).float()).float()
+    refs = {"bf16": y, "gelu": bf(torch.nn.functional.gelu(y)).float(), "res_bf16": bf(y + bf(res).float()).float()}
+    outs = {}
+    for name, f in (("t128", ops.GEMM_TILE128), ("pp", ops.GEMM_TILE256PP)):
+        o = {}
+        Cb = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, Cb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, flags=ops.GEMM_ROUND | f)
+        o["bf16"] = Cb
+        Cg = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, Cg, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, flags=ops.GEMM_ROUND | ops.GEMM_GELU | f)
+        o["gelu"] = Cg
+        rb = bf(res).to(DEV)
+        ops.gemm(Ad, Wd, rb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rb, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_bf16"] = rb
+        torch.cuda.synchronize()
+        outs[name] = {k: v.float().cpu() for k, v in o.items()}
+    for kind, ref in refs.items():
+        got = outs["pp"][kind]
+        assert not torch.isnan(got).any(), kind
+        assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max(), kind
+        assert torch.equal(got, outs["t128"][kind]), kind
+    # a strided C view: the columns past N (inside ldc) must stay untouched
+    big = torch.full((M, N + 24), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(Ad, Wd, big[:, :N], M, N, K, lda=K, ldb=K, ldc=N + 24, bias=bd, flags=ops.GEMM_ROUND | ops.GEMM_TILE256PP)
+    torch.cuda.synchronize()
+    assert torch.equal(big[:, :N].float().cpu(), outs["pp"]["bf16"])
+    assert bool((big[:, N:] == 7.0).all())
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 16, 8), (5, 1000, 1280), (64, 1281 - 1, 5120), (100, 3840, 1280),
                                    (128, 200, 64)])
 def test_gemm_skinny_decode_path(M, N, K):
