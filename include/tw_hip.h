@@ -142,6 +142,24 @@ int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint
                         const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids, int col,
                         int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin, int no_ts, int max_initial,
                         int* last_ts, tw_stream_t stream);
+/* Temperature fallback (HF generate_with_fallback, generation_whisper.py:970-1090; _need_fallback :1243-1290;
+ * _retrieve_avg_logprobs :1958-1975; WhisperNoSpeechDetection logits_process.py:2050-2112).
+ * tw_select_sample[_ts]: tw_greedy_select[_ts] with ctl = device int32[3] {bits of 1/T, seed lo, seed hi}
+ * (1/T == 0: argmax; else Gumbel-max sampling over the processed row, i.e. multinomial(softmax(x/T)) with
+ * a counter-based hash RNG keyed by (seed, b, col, id) -- not torch's RNG stream) and, when sum_logp !=
+ * NULL, sum_logp[b] += log_softmax(processed row)[chosen] for rows not yet finished (the eos step
+ * included).  B, V < 2^21.
+ * tw_token_logprob: out[b] = log_softmax(logits[b*ld + 0..V))[token] (the no-speech probability is
+ * exp(out) at the <|startoftranscript|> position). */
+int tw_select_sample(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                     const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
+                     int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col, const uint32_t* ctl,
+                     float* sum_logp, tw_stream_t stream);
+int tw_select_sample_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                        const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids, int col,
+                        int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin, int no_ts, int max_initial,
+                        int* last_ts, const uint32_t* ctl, float* sum_logp, tw_stream_t stream);
+int tw_token_logprob(const void* logits, int64_t ld, int B, int V, int token, float* out, tw_stream_t stream);
 int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
                   int out_dtype, int B, int D, const int* t_dev, tw_stream_t stream);
 int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n,

@@ -11,6 +11,15 @@
 //    generated step), finished rows forced to eos (= pad), token written to the id matrix and
 //    to the next step's input vector, finished flag updated.  Ties resolve to the lowest id
 //    (torch.argmax).
+//  * tw_select_sample[_ts]: the same selection with the temperature-fallback extensions of HF
+//    generate_with_fallback (generation_whisper.py:970-1090): sampling at temperature T by the
+//    Gumbel-max trick over the processed row (argmax of x/T + G, G = -log(-log U), U from a
+//    counter-based hash of (seed, row, column, id): distributed as multinomial(softmax(x/T)),
+//    not torch's RNG stream), and the running sum of log-softmax(processed row)[chosen] that
+//    _retrieve_avg_logprobs computes (scores * T undoes the temperature warper).  T and the
+//    seed live in a device control word, so one captured decode graph serves every fallback
+//    temperature.
+//  * tw_token_logprob: log-softmax of a raw logits row at one id (WhisperNoSpeechDetection).
 #include "common.h"
 
 namespace {
@@ -123,43 +132,105 @@ struct SelP {
   int64_t* next;              // [B] next-step input ids
   const int* t_dev;           // nullable: col = *t_dev + col, begin mask applied when col == begin_col
   int begin_col;
+  const uint32_t* ctl;        // nullable: [0] = bits of 1/T (0: greedy), [1], [2] = seed lo, hi
+  float* sum_logp;            // nullable: += log-prob of the chosen token while the row is live
 };
+
+// (max, sum exp(x - max)) pairs: running logsumexp
+__device__ __forceinline__ void lse_add(float& m, float& s, float x) {
+  if (x > m) { s = s * __expf(m - x) + 1.f; m = x; }
+  else s += __expf(x - m);
+}
+__device__ __forceinline__ void lse_merge(float& m, float& s, float om, float os) {
+  const float mx = fmaxf(m, om);
+  s = (mx == -INFINITY) ? 0.f : s * __expf(m - mx) + os * __expf(om - mx);
+  m = mx;
+}
+__device__ __forceinline__ float lse_val(float m, float s) { return m == -INFINITY ? -INFINITY : m + __logf(s); }
+
+// Gumbel(0,1) noise of token v at (row b, column col): splitmix64 of a distinct 64-bit key
+// (b, col, v < 2^21 each) -> 24-bit uniform in (0, 1)
+__device__ __forceinline__ float gumbel(uint64_t seed, int b, int col, int v) {
+  uint64_t x = seed + 0x9E3779B97F4A7C15ull *
+                          ((((uint64_t)(uint32_t)b) << 42) ^ (((uint64_t)(uint32_t)col) << 21) ^ (uint64_t)(uint32_t)v);
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = ((float)(x >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  return -__logf(-__logf(u));
+}
+
+__device__ __forceinline__ void read_ctl(const uint32_t* ctl, float& inv_t, uint64_t& seed) {
+  inv_t = ctl ? __uint_as_float(ctl[0]) : 0.f;
+  seed = ctl ? ((uint64_t)ctl[2] << 32 | ctl[1]) : 0ull;
+}
+
+// block (256 threads) argmax with lowest-id ties, result broadcast to thread 0's registers
+__device__ __forceinline__ void block_argmax(float& v, int& i, float (*sv)[4], int (*si)[4], int slot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+  if (lane == 0) { sv[slot][wave] = v; si[slot][wave] = i; }
+  __syncthreads();
+  if (tid == 0)
+    for (int w = 1; w < 4; ++w)
+      if (sv[slot][w] > v || (sv[slot][w] == v && si[slot][w] < i)) { v = sv[slot][w]; i = si[slot][w]; }
+}
+__device__ __forceinline__ void block_lse(float& m, float& s, float (*sv)[4], int slot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o, 64), __shfl_xor(s, o, 64));
+  if (lane == 0) { sv[slot][wave] = m; sv[slot + 1][wave] = s; }
+  __syncthreads();
+  if (tid == 0)
+    for (int w = 1; w < 4; ++w) lse_merge(m, s, sv[slot][w], sv[slot + 1][w]);
+}
 
 __device__ __forceinline__ bool bit(const uint32_t* m, int v) { return m && ((m[v >> 5] >> (v & 31)) & 1u); }
 
 __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
-  __shared__ float bv[4];
-  __shared__ int bi[4];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float sv[4][4];
+  __shared__ int si[4][4];
+  const int b = blockIdx.x, tid = threadIdx.x;
   if (p.t_dev) {
     p.col += *p.t_dev;
     p.apply_begin = p.col == p.begin_col;
   }
+  float inv_t;
+  uint64_t seed;
+  read_ctl(p.ctl, inv_t, seed);
+  const bool sample = inv_t > 0.f;
   const bf16* row = p.logits + b * p.ld;
-  float best = -INFINITY;
-  int besti = 0x7fffffff;
+  float best = -INFINITY, sbest = -INFINITY, m = -INFINITY, se = 0.f;
+  int besti = 0x7fffffff, sbesti = 0x7fffffff;
   for (int v = tid; v < p.V; v += 256) {
     float x = bf2f(row[v]);
     if (bit(p.suppress, v) || (p.apply_begin && bit(p.begin, v))) x = -INFINITY;
     if (x > best || (x == best && v < besti)) { best = x; besti = v; }
+    if (x > -INFINITY) {
+      lse_add(m, se, x);
+      if (sample) {
+        const float g = x * inv_t + gumbel(seed, b, p.col, v);
+        if (g > sbest || (g == sbest && v < sbesti)) { sbest = g; sbesti = v; }
+      }
+    }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(besti, o, 64);
-    if (ov > best || (ov == best && oi < besti)) { best = ov; besti = oi; }
-  }
-  if (lane == 0) { bv[wave] = best; bi[wave] = besti; }
-  __syncthreads();
+  block_argmax(best, besti, sv, si, 0);
+  if (sample) block_argmax(sbest, sbesti, sv, si, 1);
+  if (p.sum_logp) block_lse(m, se, sv, 2);
   if (tid == 0) {
-    for (int w = 1; w < 4; ++w)
-      if (bv[w] > best || (bv[w] == best && bi[w] < besti)) { best = bv[w]; besti = bi[w]; }
-    if (besti == 0x7fffffff) besti = 0;            // every logit masked / NaN: id 0 (torch argmax of all -inf)
+    int pick = sample ? sbesti : besti;
+    if (pick == 0x7fffffff) pick = 0;              // every logit masked / NaN: id 0 (torch argmax of all -inf)
     const bool fin = p.done[b] != 0;
-    const int64_t tok = fin ? p.eos : (int64_t)besti;
+    const int64_t tok = fin ? p.eos : (int64_t)pick;
     p.ids[b * p.ld_ids + p.col] = tok;
     p.next[b] = tok;
     p.done[b] = (fin || tok == p.eos) ? 1 : 0;
+    if (p.sum_logp && !fin) p.sum_logp[b] += bf2f(row[pick]) - lse_val(m, se);
   }
 }
 
@@ -182,9 +253,17 @@ struct SelTsP {
 __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   __shared__ float sv[4][3];
   __shared__ int si[4][2];
+  __shared__ float sx[4][4];
+  __shared__ int sxi[4][4];
+  __shared__ float s_tm, s_ts, s_bt, s_bs;
+  __shared__ int s_mask_text;
   SelP& p = q.s;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (p.t_dev) p.col += *p.t_dev;
+  float inv_t;
+  uint64_t seed;
+  read_ctl(p.ctl, inv_t, seed);
+  const bool sample = inv_t > 0.f;
   const bool first = p.col == q.begin_col;
   const int64_t* idr = p.ids + b * p.ld_ids;
   const bool has1 = p.col - 1 >= q.begin_col, has2 = p.col - 2 >= q.begin_col;
@@ -194,21 +273,29 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   const int lim = lt < 0 ? q.ts_begin : ((last_ts && !pen_ts) ? lt : lt + 1);
   const int ts_hi = (first && q.max_initial >= 0) ? q.ts_begin + q.max_initial : 0x7fffffff;
   const bf16* row = p.logits + b * p.ld;
-  float bt = -INFINITY, bs = -INFINITY, se = 0.f;        // best text, best timestamp, sum exp(ts - bs)
-  int it = 0x7fffffff, is = 0x7fffffff;
-  for (int v = tid; v < p.V; v += 256) {
-    float x = bf2f(row[v]);
+  // eligibility of id v before the "timestamp mass wins" rule
+  auto masked = [&](int v) -> bool {
     bool m = bit(p.suppress, v) || (first && bit(p.begin, v)) || v == q.no_ts;
     if (v >= q.ts_begin) {
       if (last_ts && pen_ts) m = true;
       if (v < lim || v > ts_hi) m = true;
-      if (!m && x > -INFINITY) {
-        if (x > bs) { se = se * __expf(bs - x) + 1.f; bs = x; is = v; }
-        else { se += __expf(x - bs); if (x == bs && v < is) is = v; }
-      }
+    } else if ((last_ts && !pen_ts && v < p.eos) || first) {
+      m = true;
+    }
+    return m;
+  };
+  float bt = -INFINITY, bs = -INFINITY, se = 0.f;        // best text, best timestamp, sum exp(ts - bs)
+  float tm = -INFINITY, tse = 0.f;                       // text logsumexp (for the log-prob)
+  int it = 0x7fffffff, is = 0x7fffffff;
+  for (int v = tid; v < p.V; v += 256) {
+    const float x = bf2f(row[v]);
+    if (masked(v) || !(x > -INFINITY)) continue;
+    if (v >= q.ts_begin) {
+      if (x > bs) { se = se * __expf(bs - x) + 1.f; bs = x; is = v; }
+      else { se += __expf(x - bs); if (x == bs && v < is) is = v; }
     } else {
-      if ((last_ts && !pen_ts && v < p.eos) || first) m = true;
-      if (!m && (x > bt || (x == bt && v < it))) { bt = x; it = v; }
+      if (x > bt || (x == bt && v < it)) { bt = x; it = v; }
+      lse_add(tm, tse, x);
     }
   }
   // wave reduction: text (max, argmin idx), timestamps (max, argmin idx, rescaled sum)
@@ -222,8 +309,12 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
     if (obs > bs || (obs == bs && ois < is)) is = ois;
     bs = mx;
     se = ns;
+    lse_merge(tm, tse, __shfl_xor(tm, o, 64), __shfl_xor(tse, o, 64));
   }
-  if (lane == 0) { sv[wave][0] = bt; sv[wave][1] = bs; sv[wave][2] = se; si[wave][0] = it; si[wave][1] = is; }
+  if (lane == 0) {
+    sv[wave][0] = bt; sv[wave][1] = bs; sv[wave][2] = se; si[wave][0] = it; si[wave][1] = is;
+    sx[0][wave] = tm; sx[1][wave] = tse;
+  }
   __syncthreads();
   if (tid == 0) {
     for (int w = 1; w < 4; ++w) {
@@ -235,20 +326,67 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
       if (obs > bs || (obs == bs && ois < is)) is = ois;
       bs = mx;
       se = ns;
+      lse_merge(tm, tse, sx[0][w], sx[1][w]);
     }
-    int best;
     const float ts_lse = bs == -INFINITY ? -INFINITY : bs + __logf(se);
-    if (bs > -INFINITY && ts_lse > bt) best = is;                    // timestamp mass wins: text masked
+    s_mask_text = (bs > -INFINITY && ts_lse > bt) ? 1 : 0;   // timestamp mass wins: text masked
+    s_tm = tm; s_ts = tse; s_bt = bt; s_bs = bs;
+    sv[0][2] = se;
+    si[0][0] = it; si[0][1] = is;
+  }
+  __syncthreads();
+  const bool mask_text = s_mask_text != 0;
+  int spick = 0x7fffffff;
+  if (sample) {                                          // second pass: Gumbel-max over the processed row
+    float sb = -INFINITY;
+    for (int v = tid; v < p.V; v += 256) {
+      const float x = bf2f(row[v]);
+      if (masked(v) || !(x > -INFINITY) || (mask_text && v < q.ts_begin)) continue;
+      const float g = x * inv_t + gumbel(seed, b, p.col, v);
+      if (g > sb || (g == sb && v < spick)) { sb = g; spick = v; }
+    }
+    block_argmax(sb, spick, sx, sxi, 2);
+  }
+  if (tid == 0) {
+    bt = s_bt; bs = s_bs; it = si[0][0]; is = si[0][1];
+    const float ts_l = lse_val(bs, sv[0][2]);
+    int best;
+    if (mask_text) best = is;
     else if (bt >= bs && it != 0x7fffffff) best = it;                 // text ids < timestamp ids: ties -> text
     else if (is != 0x7fffffff) best = is;
     else best = 0;
+    if (sample) best = spick == 0x7fffffff ? best : spick;
     const bool fin = p.done[b] != 0;
     const int64_t tok = fin ? p.eos : (int64_t)best;
     p.ids[b * p.ld_ids + p.col] = tok;
     p.next[b] = tok;
     p.done[b] = (fin || tok == p.eos) ? 1 : 0;
     if (!fin && tok >= q.ts_begin) q.last_ts[b] = (int)tok;
+    if (p.sum_logp && !fin) {
+      float lse = ts_l;
+      if (!mask_text) {
+        float m = s_tm, ss = s_ts;
+        if (bs > -INFINITY) lse_merge(m, ss, bs, sv[0][2]);
+        lse = lse_val(m, ss);
+      }
+      p.sum_logp[b] += bf2f(row[best]) - lse;
+    }
   }
+}
+
+// out[b] = log_softmax(logits[b, :V])[token]   (fp32 of the bf16 row)
+__global__ __launch_bounds__(256) void token_logprob_kernel(const bf16* __restrict__ logits, int64_t ld, int V,
+                                                            int token, float* __restrict__ out) {
+  __shared__ float sv[4][4];
+  const int b = blockIdx.x;
+  const bf16* row = logits + b * ld;
+  float m = -INFINITY, s = 0.f;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    const float x = bf2f(row[v]);
+    if (x > -INFINITY) lse_add(m, s, x);
+  }
+  block_lse(m, s, sv, 0);
+  if (threadIdx.x == 0) out[b] = bf2f(row[token]) - lse_val(m, s);
 }
 
 // x[b] = tok[ids[b]] + pos[*t_dev]   (decoder input embedding of step t, HF modeling_whisper.py:720-735)
@@ -291,8 +429,38 @@ extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V,
   q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
   q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
+  q.s.ctl = nullptr; q.s.sum_logp = nullptr;
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
   hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                                   const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids,
+                                   int col, int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin,
+                                   int no_ts, int max_initial, int* last_ts, const uint32_t* ctl, float* sum_logp,
+                                   hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  if (V <= 0 || ld < V || !done || !ids || !next_ids || !last_ts || ts_begin <= eos || ts_begin > V) return TW_EINVAL;
+  if (B >= (1 << 21) || V >= (1 << 21)) return TW_EUNSUPPORTED;     // RNG key widths
+  SelTsP q;
+  q.s.logits = (const bf16*)logits; q.s.ld = ld; q.s.V = V;
+  q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
+  q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
+  q.s.t_dev = t_dev; q.s.begin_col = begin_col;
+  q.s.ctl = ctl; q.s.sum_logp = sum_logp;
+  q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
+  hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_token_logprob(const void* logits, int64_t ld, int B, int V, int token, float* out,
+                                hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  if (V <= 0 || ld < V || token < 0 || token >= V || !out) return TW_EINVAL;
+  hipLaunchKernelGGL(token_logprob_kernel, dim3(B), dim3(256), 0, stream, (const bf16*)logits, ld, V, token, out);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
@@ -355,6 +523,25 @@ extern "C" int tw_greedy_select(const void* logits, int64_t ld, int B, int V, co
   p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
+  p.ctl = nullptr; p.sum_logp = nullptr;
+  hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_select_sample(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                                const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
+                                int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col,
+                                const uint32_t* ctl, float* sum_logp, hipStream_t stream) {
+  if (B <= 0) return TW_OK;
+  if (V <= 0 || ld < V || !done || !ids || !next_ids) return TW_EINVAL;
+  if (B >= (1 << 21) || V >= (1 << 21)) return TW_EUNSUPPORTED;     // RNG key widths
+  SelP p;
+  p.logits = (const bf16*)logits; p.ld = ld; p.V = V;
+  p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
+  p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
+  p.t_dev = t_dev; p.begin_col = begin_col;
+  p.ctl = ctl; p.sum_logp = sum_logp;
   hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;

@@ -41,6 +41,9 @@ SIGNATURES = {
     "tw_decode_attn": [P, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, I32, P, I32, F32, P],
     "tw_greedy_select": [P, I64, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P],
     "tw_greedy_select_ts": [P, I64, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P],
+    "tw_select_sample": [P, I64, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P, P, P],
+    "tw_select_sample_ts": [P, I64, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P, P, P],
+    "tw_token_logprob": [P, I64, I32, I32, I32, P, P],
     "tw_embed_step": [P, P, I32, P, I32, P, I32, I32, I32, P, P],
     "tw_kv_append": [P, I64, P, I64, I64, I32, I32, P, P],
     "tw_step_advance": [P, I32, P],

@@ -152,8 +152,8 @@ class _Select:
     """Per-step token selection into ids[:, t+1] (t read on the device): HF SuppressTokens,
     SuppressTokensAtBegin and, with timestamps, WhisperTimeStampLogitsProcessor + argmax."""
 
-    def __init__(self, gc, B, V, T_max, P, dev, timestamps):
-        self.V, self.P, self.ts = V, P, timestamps
+    def __init__(self, gc, B, V, T_max, P, dev, timestamps, track=False):
+        self.V, self.P, self.ts, self.track = V, P, timestamps, track
         self.eos = int(gc.eos_token_id)
         self.sup = F.token_bitmask(gc.suppress_tokens or [], V, dev)
         self.beg = F.token_bitmask(gc.begin_suppress_tokens or [], V, dev)
@@ -163,16 +163,33 @@ class _Select:
         self.no_ts = int(gc.no_timestamps_token_id)
         mi = gc.max_initial_timestamp_index if "max_initial_timestamp_index" in gc else None
         self.max_initial = -1 if mi is None else int(mi)
+        # temperature fallback: sampling control word (1/T, seed) read on the device, so a captured
+        # graph serves every temperature; running log-prob of the chosen tokens
+        self.ctl = torch.zeros(3, dtype=torch.int32, device=dev) if track else None
+        self.sum_logp = torch.zeros(B, dtype=torch.float32, device=dev) if track else None
 
-    def reset(self, prompt):
+    def reset(self, prompt, temperature=0.0, seed=0):
         self.ids.fill_(self.eos)
         self.ids[:, :self.P] = prompt
         self.done.zero_()
         self.last_ts.fill_(-1)
+        if self.track:
+            self.sum_logp.zero_()
+            F.sample_ctl(temperature, seed, self.ctl)
+        elif temperature:
+            raise ValueError("sampling needs a tracking selector (track=True)")
 
     def __call__(self, sess):
         B = sess.B
-        if self.ts:
+        if self.track:
+            if self.ts:
+                F.select_sample_ts(sess.logits, sess.m.Vp, B, self.V, self.sup, self.beg, self.eos, self.done, self.ids,
+                                   1, sess.cur, self.last_ts, self.P, self.ctl, self.sum_logp, ts_begin=self.no_ts + 1,
+                                   no_ts=self.no_ts, max_initial=self.max_initial, t_dev=sess.t_dev)
+            else:
+                F.select_sample(sess.logits, sess.m.Vp, B, self.V, self.sup, self.beg, False, self.eos, self.done,
+                                self.ids, 1, sess.cur, self.ctl, self.sum_logp, t_dev=sess.t_dev, begin_col=self.P)
+        elif self.ts:
             F.greedy_select_ts(sess.logits, sess.m.Vp, B, self.V, self.sup, self.beg, self.eos, self.done, self.ids, 1,
                                sess.cur, self.last_ts, self.P, ts_begin=self.no_ts + 1, no_ts=self.no_ts,
                                max_initial=self.max_initial, t_dev=sess.t_dev)
@@ -185,25 +202,31 @@ class _Decoder:
     """One greedy decode of B windows with a fixed prompt; reusable across windows (long-form):
     the captured step graph stays valid because every buffer it touches is reused in place."""
 
-    def __init__(self, model, gc, B, Tk, P, max_length, timestamps, use_graph):
+    def __init__(self, model, gc, B, Tk, P, max_length, timestamps, use_graph, track=False):
         self.m, self.P, self.T_max, self.use_graph = model, P, max_length, use_graph
         self.sess = None
-        self.sel = _Select(gc, B, model.config.vocab_size, max_length, P, model.device, timestamps)
+        self.sel = _Select(gc, B, model.config.vocab_size, max_length, P, model.device, timestamps, track)
         self.B, self.Tk = B, Tk
+        self.ns_logp = torch.zeros(B, dtype=torch.float32, device=model.device) if track else None
 
-    def run(self, enc16, prompt):
-        """prompt: int64 [B, P] (device) -> generated ids [B, L] (device), HF trimming."""
+    def run(self, enc16, prompt, temperature=0.0, seed=0, no_speech=None):
+        """prompt: int64 [B, P] (device) -> generated ids [B, L] (device), HF trimming.
+        no_speech = (sot_position, token): log-softmax of the raw logits at the <|startoftranscript|>
+        position for that token goes to self.ns_logp (WhisperNoSpeechDetection)."""
         sel, P = self.sel, self.P
         if self.sess is None:
             self.sess = DecodeSession(self.m, enc16, self.B, self.Tk, self.T_max)
         else:
             self.sess.set_encoder(enc16)
         sess = self.sess
-        sel.reset(prompt)
+        sel.reset(prompt, temperature, seed)
         sess.t_dev.zero_()
+        V = self.m.config.vocab_size
         for t in range(P - 1):                                   # prefill the cache with the prompt
             sess.cur.copy_(sel.ids[:, t])
             sess.step()
+            if no_speech is not None and t == no_speech[0]:
+                F.token_logprob(sess.logits, self.m.Vp, self.B, V, no_speech[1], self.ns_logp)
         sess.cur.copy_(sel.ids[:, P - 1])
         if self.use_graph and sess.graph is None:
             sess.capture(sel)
@@ -213,6 +236,8 @@ class _Decoder:
                 sess.graph.replay()
             else:
                 sess.step(sel)
+            if no_speech is not None and t == P - 1 and no_speech[0] == P - 1:
+                F.token_logprob(sess.logits, self.m.Vp, self.B, V, no_speech[1], self.ns_logp)
             t += 1
             if (t - P) % 8 == 7 and bool(sel.done.all()):
                 break
@@ -254,8 +279,11 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     from .config import GenerationConfig
     if num_beams not in (None, 1):
         raise NotImplementedError("tw generate: greedy only (num_beams=1, as every reference call site)")
-    if kw.get("do_sample") or kw.get("temperature") not in (None, 0, 0.0):
-        raise NotImplementedError("tw generate: sampling / temperature fallback is not built (greedy only)")
+    temperature = kw.get("temperature")
+    fb = dict(temperature=temperature if temperature is not None else 0.0,
+              compression_ratio_threshold=kw.get("compression_ratio_threshold"),
+              logprob_threshold=kw.get("logprob_threshold"), no_speech_threshold=kw.get("no_speech_threshold"),
+              condition_on_prev_tokens=bool(kw.get("condition_on_prev_tokens") or False), seed=int(kw.get("seed", 0)))
     gc = model.generation_config if model.generation_config is not None else GenerationConfig()
     if not isinstance(gc, GenerationConfig):
         gc = GenerationConfig(gc)
@@ -266,7 +294,12 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     window = 2 * cfg.max_source_positions                     # 3000 feature frames = 30 s
     if encoder_outputs is None and input_features is not None and input_features.shape[-1] > window:
         return _longform(model, gc, input_features, attention_mask, language, task, max_length, max_new_tokens,
-                         use_graph, window, kw.get("_trace"))
+                         use_graph, window, kw.get("_trace"), **fb)
+    if kw.get("do_sample") or fb["temperature"] not in (0, 0.0) or fb["logprob_threshold"] is not None \
+            or fb["compression_ratio_threshold"] is not None or fb["no_speech_threshold"] is not None:
+        # the reference applies fallback / thresholds to long-form inputs only (run_eval.py:659-685)
+        raise NotImplementedError("tw generate: temperature fallback and thresholds apply to long-form (> 30 s) "
+                                  "inputs, as in the reference; short-form decoding is greedy")
     if encoder_outputs is not None:
         enc = encoder_outputs.last_hidden_state if hasattr(encoder_outputs, "last_hidden_state") else encoder_outputs[0]
         B, Tk = enc.shape[0], enc.shape[1]
@@ -294,39 +327,128 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     return dec.run(enc16, prompt.to(model.device))
 
 
+def compression_ratio(tokens, vocab_size):
+    """HF _retrieve_compression_ratio (generation_whisper.py:1949-1956): raw token bytes (little-endian,
+    int(log2(V)/8)+1 bytes each) over their zlib-compressed length."""
+    import math
+    import zlib
+    n = int(math.log2(vocab_size) / 8) + 1
+    raw = b"".join(int(t).to_bytes(n, "little") for t in tokens)
+    return len(raw) / len(zlib.compress(raw))
+
+
+def need_fallback(tokens, avg_logprob, no_speech_prob, vocab_size, compression_ratio_threshold=None,
+                  logprob_threshold=None, no_speech_threshold=None):
+    """HF _need_fallback (generation_whisper.py:1243-1290) -> (needs_fallback, should_skip)."""
+    needs, skip = False, False
+    if compression_ratio_threshold is not None and compression_ratio(tokens, vocab_size) > compression_ratio_threshold:
+        needs = True
+    if logprob_threshold is not None and avg_logprob < logprob_threshold:
+        needs = True
+    if no_speech_threshold is not None and logprob_threshold is not None:
+        if avg_logprob < logprob_threshold and no_speech_prob > no_speech_threshold:
+            needs, skip = False, True
+    return needs, skip
+
+
 def _longform(model, gc, feats, attention_mask, language, task, max_length, max_new_tokens, use_graph, window,
-              trace=None):
-    """HF sequential long-form generate (generation_whisper.py step 6; temperature 0, no fallback
-    thresholds, no previous-text conditioning): per input, 30 s windows from `seek`, greedy with
-    timestamp rules, trailing eos/pad trimmed, segments split at consecutive timestamps, seek
-    advanced by the last timestamp (or the whole window on a single-timestamp ending); returns
-    the concatenated segment tokens, right-padded with pad."""
+              trace=None, temperature=0.0, compression_ratio_threshold=None, logprob_threshold=None,
+              no_speech_threshold=None, condition_on_prev_tokens=False, seed=0):
+    """HF sequential long-form generate (generation_whisper.py step 6): per input, 30 s windows from
+    `seek`; each window decoded with timestamp rules at the first temperature of `temperature` and
+    re-decoded at the next one while HF's fallback test fails (compression ratio of the token bytes,
+    average log-prob of the processed scores, no-speech probability at <|startoftranscript|> -> skip
+    the window); trailing eos/pad trimmed, segments split at consecutive timestamps, seek advanced
+    by the last timestamp (or the whole window on a single-timestamp ending).  With
+    condition_on_prev_tokens (and the accepted temperature < 0.5) the next window's prompt is
+    <|startofprev|> + the last max_target_positions // 2 - 1 tokens of the clip's segments (a
+    segment's closing timestamp of a double-timestamp ending dropped) + the task prompt.  Returns
+    the concatenated segment tokens, right-padded with pad.  Sampled windows draw from
+    softmax(x / T) with the engine's counter-based RNG (seeded by `seed`, the clip, the window and
+    the fallback index), not torch's RNG stream."""
     cfg = model.config
     dev = model.device
     feats = feats.to(dev, torch.float32)
     B, nmel, T = feats.shape
     lens = attention_mask.sum(-1).tolist() if attention_mask is not None else [T] * B
-    prompt = torch.tensor(build_prompt(gc, language, task, True), dtype=torch.int64, device=dev)[None]
-    P = prompt.shape[1]
-    if max_new_tokens is not None:
-        max_length = P + int(max_new_tokens)
-    max_length = min(int(max_length or gc.max_length or cfg.max_target_positions), cfg.max_target_positions)
+    init = build_prompt(gc, language, task, True)
+    temps = tuple(temperature) if isinstance(temperature, (list, tuple)) else (temperature,)
+    track = (logprob_threshold is not None or no_speech_threshold is not None or any(t and t > 0 for t in temps)
+             or len(temps) > 1)
     eos, pad = int(gc.eos_token_id), int(gc.pad_token_id if gc.pad_token_id is not None else gc.eos_token_id)
     ts_begin = int(gc.no_timestamps_token_id) + 1
-    dec = _Decoder(model, gc, 1, cfg.max_source_positions, P, max_length, True, use_graph)
+    ns_token = int(gc.no_timestamps_token_id) - 1
+    V = cfg.vocab_size
+    cut_off = cfg.max_target_positions // 2 - 1
+    prev_sot = gc.get("prev_sot_token_id") if hasattr(gc, "get") else None
+    if prev_sot is None:
+        sup = list(gc.suppress_tokens or [])
+        prev_sot = sup[-2] if len(sup) >= 2 else None
+    decoders = {}
+
+    def decoder(P, ml):
+        if (P, ml) not in decoders:
+            decoders[(P, ml)] = _Decoder(model, gc, 1, cfg.max_source_positions, P, ml, True, use_graph, track)
+        return decoders[(P, ml)]
+
     seg_in = torch.zeros(1, nmel, window, dtype=torch.float32, device=dev)
     outs = []
     for b in range(B):
         Tb = int(lens[b])
-        seek, out = 0, []
+        seek, out, segments, nwin = 0, [], [], 0
+        cond = bool(condition_on_prev_tokens)
         while seek < Tb:
             n = min(window, Tb - seek)
             seg_in.zero_()
             seg_in[0, :, :n] = feats[b, :, seek:seek + n]
             enc16 = model.encode(model.conv_input(seg_in))
-            seq = dec.run(enc16, prompt)[0].tolist()
-            if trace is not None:
-                trace.append(dict(b=b, seek=seek, n=n, raw=list(seq)))
+            prompt = list(init)
+            if cond and segments and prev_sot is not None:
+                prev = []
+                for st in segments:
+                    prev.extend(st[:-1] if len(st) > 2 and st[-2] >= ts_begin else st)
+                prompt = [int(prev_sot)] + prev[-cut_off:] + init
+            P = len(prompt)
+            if max_new_tokens is not None:
+                ml = P + int(max_new_tokens)
+            else:
+                ml = int(max_length or gc.max_length or cfg.max_target_positions)
+            ml = min(ml, cfg.max_target_positions)
+            if P >= ml:
+                raise ValueError(f"prompt of {P} tokens leaves no room below max_length {ml}")
+            dec = decoder(P, ml)
+            ptens = torch.tensor([prompt], dtype=torch.int64, device=dev)
+            ns = (P - len(init), ns_token) if no_speech_threshold is not None else None
+            skip, t_acc, seq = False, temps[0], []
+            for fi, temp in enumerate(temps):
+                raw = dec.run(enc16, ptens, temperature=temp or 0.0,
+                              seed=(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1),
+                              no_speech=ns)[0].tolist()
+                cand = list(raw)
+                if cand and cand[-1] == pad:                     # HF: padding removed except one eos
+                    k = len(cand)
+                    while k > 1 and cand[k - 2] == pad:
+                        k -= 1
+                    cand = cand[:k] if pad == eos else cand[:k - 1]
+                needs = False
+                if track or compression_ratio_threshold is not None:
+                    avg = float(dec.sel.sum_logp[0]) / max(len(cand), 1) if track else 0.0
+                    nsp = float(torch.exp(dec.ns_logp[0])) if ns is not None else 0.0
+                    needs, skip = need_fallback(cand, avg, nsp, V, compression_ratio_threshold, logprob_threshold,
+                                                no_speech_threshold)
+                    if trace is not None:
+                        trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw),
+                                          avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip))
+                elif trace is not None:
+                    trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw)))
+                seq, t_acc = raw, temp
+                if not needs:
+                    break
+            nwin += 1
+            cond = bool(condition_on_prev_tokens) and (t_acc is None or t_acc < 0.5)
+            if skip:
+                seek += n
+                continue
             if seek + window < Tb and seq and seq[-1] == eos:   # not the last window: cut a predicted eos
                 seq = seq[:-1]
             if seq and seq[-1] == pad:                          # trailing pads (pad == eos keeps one)
@@ -340,6 +462,7 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
             segs, off = retrieve_segment(seq, n, ts_begin)
             for sgm in segs:
                 out.extend(sgm)
+                segments.append(list(sgm))
             seek += off if off > 0 else n          # a closing <|0.00|> pair would not advance: take the window
         outs.append(out)
     L = max((len(o) for o in outs), default=0)

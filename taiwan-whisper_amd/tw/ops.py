@@ -315,6 +315,60 @@ def greedy_select_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids
          _stream())
 
 
+def select_sample(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids, ctl,
+                  sum_logp, t_dev=None, begin_col=-1):
+    """greedy_select + temperature sampling (ctl: int32[3] = bits(1/T), seed lo, hi; 1/T = 0 -> argmax)
+    + running log-prob of the chosen token (sum_logp: float32[B])."""
+    assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
+    _need(sum_logp, B, "select sum_logp")
+    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
+    assert done.dtype == torch.uint8
+    _need(logits, (B - 1) * ld + V, "select logits")
+    _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "select ids")
+    _need(done, B, "select done"); _need(next_ids, B, "select next")
+    call("tw_select_sample", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
+         int(eos), done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev),
+         int(begin_col), ctl.data_ptr(), sum_logp.data_ptr(), _stream())
+
+
+def select_sample_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids, col, next_ids, last_ts, begin_col,
+                     ctl, sum_logp, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
+    assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
+    _need(sum_logp, B, "select sum_logp")
+    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
+    assert done.dtype == torch.uint8 and last_ts.dtype == torch.int32
+    _need(logits, (B - 1) * ld + V, "select logits")
+    _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "select ids")
+    _need(done, B, "select done"); _need(next_ids, B, "select next"); _need(last_ts, B, "select last_ts")
+    call("tw_select_sample_ts", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(eos),
+         done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev), int(begin_col),
+         int(ts_begin), int(no_ts), int(max_initial if max_initial is not None else -1), last_ts.data_ptr(),
+         ctl.data_ptr(), sum_logp.data_ptr(), _stream())
+
+
+def token_logprob(logits, ld, B, V, token, out):
+    """out[b] = log_softmax(logits[b, :V])[token] (float32)."""
+    assert logits.dtype == torch.bfloat16 and out.dtype == torch.float32
+    _need(logits, (B - 1) * ld + V, "token_logprob logits"); _need(out, B, "token_logprob out")
+    call("tw_token_logprob", logits.data_ptr(), ld, B, V, int(token), out.data_ptr(), _stream())
+    return out
+
+
+def sample_ctl(temperature: float, seed: int, out=None):
+    """Device control word of select_sample[_ts]: [bits(1/T) (0 = greedy), seed lo, seed hi]."""
+    import struct
+    inv = 0.0 if not temperature or temperature <= 0 else 1.0 / float(temperature)
+    bits = struct.unpack("<i", struct.pack("<f", inv))[0]
+    seed = int(seed) & ((1 << 64) - 1)
+    lo, hi = seed & 0xFFFFFFFF, seed >> 32
+    vals = torch.tensor([bits, lo - (1 << 32) if lo >= 1 << 31 else lo, hi - (1 << 32) if hi >= 1 << 31 else hi],
+                        dtype=torch.int32)
+    if out is None:
+        return vals
+    out.copy_(vals)
+    return out
+
+
 def embed_step(ids, tok, pos, out, t_dev, max_pos):
     B = ids.numel()
     D = tok.shape[1]

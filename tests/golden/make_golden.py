@@ -242,11 +242,52 @@ def gen_greedy_ts(out):
     out["ts_long_ids"] = ids.numpy()
 
 
+def gen_fallback(out):
+    """HF long-form generate with previous-text conditioning (temperature 0) and with the fallback
+    thresholds at a single temperature (deterministic: no sampled retry), on the 65 s features:
+      fb_cond_ids       condition_on_prev_tokens=True
+      fb_none_ids       logprob_threshold=-1e9, no_speech_threshold=1.0   (no window fails / is skipped)
+      fb_skipall_ids    logprob_threshold=+1e9, no_speech_threshold=0.0   (every window skipped)
+      fb_ns_probs / fb_avg_logprobs: per-window no-speech probability and avg log-prob recorded from
+                        HF's WhisperNoSpeechDetection / _retrieve_avg_logprobs during the cond run."""
+    cfg = CONFIGS["micro"]
+    m = hf_model(cfg, make_weights(cfg, 1, lin_std=0.2)).eval()
+    m.generation_config = ts_generation_config()
+    lf = torch.from_numpy(longform_features())
+    am = torch.ones(1, lf.shape[-1], dtype=torch.long)
+    kw = dict(attention_mask=am, return_timestamps=True, language="zh", task="transcribe")
+    rec = {"avg": [], "ns": []}
+    orig_need = type(m)._need_fallback
+
+    def spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size, temperature):
+        scores = seek_outputs[index]["scores"]
+        rec["avg"].append(float(self._retrieve_avg_logprobs(scores, seek_sequence, temperature)))
+        from transformers.generation.logits_process import WhisperNoSpeechDetection
+        for p_ in logits_processor or []:
+            if isinstance(p_, WhisperNoSpeechDetection):
+                rec["ns"].append(float(p_.no_speech_prob[index]))
+        return orig_need(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
+                         temperature)
+    with torch.no_grad():
+        out["fb_cond_ids"] = m.generate(lf, condition_on_prev_tokens=True, temperature=0.0, **kw).numpy()
+        out["fb_none_ids"] = m.generate(lf, temperature=(0.0,), logprob_threshold=-1e9, no_speech_threshold=1.0,
+                                        **kw).numpy()
+        out["fb_skipall_ids"] = m.generate(lf, temperature=(0.0,), logprob_threshold=1e9, no_speech_threshold=0.0,
+                                           **kw).numpy()
+        type(m)._need_fallback = spy
+        try:
+            m.generate(lf, temperature=(0.0,), logprob_threshold=-1e9, no_speech_threshold=1.0, **kw)
+        finally:
+            type(m)._need_fallback = orig_need
+    out["fb_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
+    out["fb_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
+
+
 def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
     for name, fn in (("mel", gen_mel), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
-                     ("greedy_ts", gen_greedy_ts)):
+                     ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback)):
         if only and name not in only:
             continue
         out = {}

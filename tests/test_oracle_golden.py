@@ -187,3 +187,25 @@ def test_longform_matches_hf_generate():
     with torch.no_grad():
         out = greedy_ref.longform(m, lf, prompt, suppress_tokens=mg.SUPPRESS, max_initial=50)
     assert out == g["ts_long_ids"][0].tolist()
+
+
+def test_longform_fallback_and_conditioning_match_hf():
+    """Deterministic part of temperature fallback + previous-text conditioning (oracle/greedy_ref.longform)
+    == HF generate on the 65 s input: conditioned prompts (<|startofprev|> + trimmed previous segments),
+    per-window average log-probs and no-speech probabilities as HF computes them, a threshold pair no
+    window fails, and a pair that skips every window."""
+    g = load_golden("fallback")
+    mg, m, prompt = _ts_setup()
+    lf = torch.from_numpy(mg.longform_features())[0]
+    kw = dict(suppress_tokens=mg.SUPPRESS, max_initial=50)
+    with torch.no_grad():
+        cond = greedy_ref.longform(m, lf, prompt, condition_on_prev_tokens=True, **kw)
+        trace = []
+        none = greedy_ref.longform(m, lf, prompt, logprob_threshold=-1e9, no_speech_threshold=1.0, trace=trace, **kw)
+        skip = greedy_ref.longform(m, lf, prompt, logprob_threshold=1e9, no_speech_threshold=0.0, **kw)
+    assert cond == g["fb_cond_ids"][0].tolist()
+    assert cond != none                                          # conditioning changed later windows
+    assert none == g["fb_none_ids"][0].tolist()
+    assert skip == [] and g["fb_skipall_ids"].shape[1] == 0
+    np.testing.assert_allclose([t["avg_logprob"] for t in trace], g["fb_avg_logprobs"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose([t["no_speech_prob"] for t in trace], g["fb_ns_probs"], rtol=1e-3)
