@@ -19,6 +19,8 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 namespace {
 
@@ -865,6 +867,75 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
   hipLaunchKernelGGL(gemm_pp_kernel, dim3(grid), dim3(512), 0, stream, p);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-K for weight gradients (dW = dYᵀ·X: both operands MN-major, K = tokens, few output tiles):
+// the K range is cut into S chunks run as S batch entries of the 128x128 kernel into an fp32
+// workspace, then one pass sums the chunks in order and applies the epilogue
+//     C = [C +] round?(alpha * sum_s ws[s])
+// (bf16 rounding point of the autocast product as in the unsplit kernel; the fp32 sum over K is
+// regrouped by chunk).  Workspace: lazily grown per (device, stream), never freed.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t split_stride,
+                                                            float* __restrict__ C, int64_t ldc, int M, int N,
+                                                            float alpha, int round, int accum) {
+  const int n4 = N >> 2;
+  const int64_t total = (int64_t)M * n4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4) * 4;
+    const float* w = ws + (int64_t)m * N + c;
+    f32x4 a = *(const f32x4*)w;
+    for (int s = 1; s < S; ++s) a += *(const f32x4*)(w + s * split_stride);
+    float* cp = C + (int64_t)m * ldc + c;
+    f32x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = round ? rbf(alpha * a[r]) : alpha * a[r];
+    if (accum) o += *(const f32x4*)cp;
+    *(f32x4*)cp = o;
+  }
+}
+
+struct SplitWs {
+  int dev; hipStream_t stream; void* ptr; size_t bytes;
+};
+
+void* splitk_workspace(hipStream_t stream, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<SplitWs> table;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& e : table)
+    if (e.dev == dev && e.stream == stream) {
+      if (e.bytes >= bytes) return e.ptr;
+      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;    // the old block may still be read
+      (void)hipFree(e.ptr);
+      e.ptr = nullptr;
+      e.bytes = 0;
+      if (hipMalloc(&e.ptr, bytes) != hipSuccess) return nullptr;
+      e.bytes = bytes;
+      return e.ptr;
+    }
+  void* ptr = nullptr;
+  if (hipMalloc(&ptr, bytes) != hipSuccess) return nullptr;
+  table.push_back({dev, stream, ptr, bytes});
+  return ptr;
+}
+
+// S for a dW-shaped call, 0 = no split: fewer than 512 128x128 tiles, K split into S equal chunks of
+// >= 1024 until >= 512 workgroups; fp32 output, flags within {ROUND, ACCUM}.
+int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
+  if (!a_trans || !b_trans || batch != 1 || p.c_dtype != TW_F32) return 0;
+  if (p.flags & ~(F_ROUND | F_ACCUM) & 0xff) return 0;
+  if ((p.N & 3) || (p.ldc & 3) || ((uintptr_t)p.C & 15)) return 0;
+  const int64_t tiles = (int64_t)((p.M + 127) / 128) * ((p.N + 127) / 128);
+  if (tiles >= 512) return 0;
+  for (int S = 2; S <= 16; S *= 2) {
+    if (p.K % S != 0 || p.K / S < 1024) break;      // chunk tails are masked like any K tail
+    if (tiles * S >= 512) return S;
+  }
+  return 0;
+}
+
 template <bool AT, bool BT>
 void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
   if (tile == 2562 && !AT && !BT) launch_pp(p, batch, stream);
@@ -925,6 +996,33 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
     launch_skinny(p, stream);                         // decode-step GEMMs: stream W once
     TW_CHECK_LAUNCH();
     return TW_OK;
+  }
+  if (!(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
+    const int S = splitk_factor(p, batch, a_trans, b_trans);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(stream, &cap);
+    const size_t bytes = (size_t)S * M * N * sizeof(float);
+    void* ws = (S > 0 && cap == hipStreamCaptureStatusNone && bytes <= ((size_t)1 << 30))
+                   ? splitk_workspace(stream, bytes) : nullptr;
+    if (ws) {
+      GemmP q = p;
+      const int Kc = K / S;
+      q.K = Kc;
+      q.sA = (int64_t)Kc * lda;                      // A is [K][M] (lda), B is [K][N] (ldb)
+      q.sB = (int64_t)Kc * ldb;
+      q.C = ws; q.ldc = N; q.sC = (int64_t)M * N; q.c_dtype = TW_F32;
+      q.alpha = 1.f; q.flags = 0; q.bias = nullptr; q.res = nullptr; q.aux = nullptr;
+      q.epi = pick_epilogue(q, S);
+      launch<true, true, 128, 128, 2, 2, 2>(q, S, stream);
+      TW_CHECK_LAUNCH();
+      const int64_t work = (int64_t)M * (N / 4);
+      const int grid = (int)std::min<int64_t>((work + 255) / 256, 4096);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, stream, (const float*)ws, S,
+                         (int64_t)M * N, (float*)C, ldc, M, N, alpha, (flags & F_ROUND) ? 1 : 0,
+                         (flags & F_ACCUM) ? 1 : 0);
+      TW_CHECK_LAUNCH();
+      return TW_OK;
+    }
   }
   if (!a_trans && !b_trans) dispatch<false, false>(p, batch, stream, tile);
   else if (!a_trans && b_trans) dispatch<false, true>(p, batch, stream, tile);

@@ -14,6 +14,7 @@ from .profiling import KernelTimer
 F32, BF16 = 0, 1
 GEMM_BIAS, GEMM_ROUND, GEMM_GELU, GEMM_RES, GEMM_ACCUM, GEMM_AUX_OUT, GEMM_DGELU = 1, 2, 4, 8, 16, 32, 64
 GEMM_TILE128, GEMM_TILE256, GEMM_TILE256x128, GEMM_TILE256PP = 256, 512, 1024, 2048   # forced tiles (A/B benchmarking)
+GEMM_NOSPLIT = 16384   # no split-K for dW-shaped calls (A/B benchmarking)
 
 
 def _dt(t: torch.Tensor) -> int:

@@ -174,6 +174,36 @@ def test_gemm_pp_persistent_ragged(M, N, K):
     assert bool((big[:, N:] == 7.0).all())
 
 
+@pytest.mark.parametrize("N,K,M", [(1280, 1280, 28608), (2560, 1280, 8192), (264, 136, 4096), (1280, 1280, 1000)])
+def test_gemm_splitk_weight_grad(N, K, M):
+    """dW[N][K] += round(dY^T X) with dY [M][N], X [M][K] (both MN-major operands, fp32 accumulate): the
+    split-K path (few tiles, long M) against the unsplit kernel and an fp64 reference.  The chunked
+    fp32 sum may move a value across a bf16 rounding boundary (one bf16 ulp) and regroups the fp32
+    sum (2e-5 of the largest product, visible only on cancellation-dominated elements)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(N + K + M)
+    dy, x = torch.randn(M, N, generator=g) * 0.1, torch.randn(M, K, generator=g)
+    dyd, xd = bf(dy).to(DEV), bf(x).to(DEV)
+    base = torch.randn(N, K, generator=g)
+    ref = bf((bf(dy).double().T @ bf(x).double()).float()).double() + base.double()
+    outs = []
+    for f in (0, ops.GEMM_NOSPLIT):
+        dw = base.clone().to(DEV)
+        ops.gemm(dyd, xd, dw, N, K, M, lda=N, ldb=K, ldc=K, a_trans=True, b_trans=True,
+                 flags=ops.GEMM_ROUND | ops.GEMM_ACCUM | f)
+        torch.cuda.synchronize()
+        outs.append(dw.cpu())
+    prod = torch.maximum((outs[0] - base).abs(), (outs[1] - base).abs())
+    # one bf16 ulp of the larger product, plus the fp32 summation-order term that dominates
+    # cancellation-heavy (near-zero) elements: 2e-5 of the largest product
+    tol = prod * 2 ** -7 + 2e-5 * float(prod.max())
+    d = (outs[0] - outs[1]).abs()
+    bad = d > tol
+    assert not bool(bad.any()), (int(bad.sum()), float(d.max()), bad.nonzero()[:5].tolist(),
+                                 rel_err(outs[0], ref), rel_err(outs[1], ref))
+    assert rel_err(outs[0], ref) < 1e-2 and rel_err(outs[1], ref) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 16, 8), (5, 1000, 1280), (64, 1281 - 1, 5120), (100, 3840, 1280),
                                    (128, 200, 64)])
 def test_gemm_skinny_decode_path(M, N, K):
