@@ -134,6 +134,10 @@ class DistillationTrainer:
         B, Td = ids.shape
         if self.micro == 0:
             s.grad.zero_()
+        # DP: on the micro-step that syncs, each layer's gradient slice is all-reduced as soon as
+        # the backward has finished it (RCCL on its own stream, beside the remaining backward)
+        self._pending, self._reduced = [], []
+        self.bw.on_ready = self._grad_ready if (self.world > 1 and self.micro + 1 == self.accum) else None
         enc_tape = [] if self.train_encoder else None
         enc16 = s.encode(conv_in, tape=enc_tape)
         Tk = enc16.shape[0] // B
@@ -178,17 +182,37 @@ class DistillationTrainer:
         return {"loss": out3[0], "ce_loss": out3[1], "kl_loss": out3[2]}
 
     # ------------------------------------------------------------------ update
+    def _launch(self, lo, hi):
+        g = self.s.grad
+        for a in range(lo, hi, self.bucket):
+            self._pending.append(torch.distributed.all_reduce(g[a: min(hi, a + self.bucket)], group=self.pg,
+                                                              async_op=True))
+        self._reduced.append((lo, hi))
+
+    def _grad_ready(self, prefix):
+        r = self.s.grad_range(prefix)
+        if r is not None:
+            self._launch(*r)
+
     def all_reduce_grads(self):
         """DDP mean over ranks (the 1/world factor is already folded into the loss gradient):
-        bucketed SUM all-reduce of the flat fp32 gradient over RCCL."""
+        bucketed SUM all-reduce of the flat fp32 gradient over RCCL.  Ranges whose exchange already
+        started during the backward (per finished layer) are skipped; the rest (embeddings, final
+        LayerNorm, ...) is launched now, then everything is waited for."""
         if self.world == 1:
             return
-        g = self.s.grad
-        works = []
-        for lo in range(0, g.numel(), self.bucket):
-            works.append(torch.distributed.all_reduce(g[lo: lo + self.bucket], group=self.pg, async_op=True))
-        for w in works:
+        done = sorted(getattr(self, "_reduced", []))
+        pos = 0
+        if not hasattr(self, "_pending"):
+            self._pending = []
+        for lo, hi in done + [(self.s.grad.numel(), self.s.grad.numel())]:
+            if lo > pos:
+                self._launch(pos, lo)
+            pos = max(pos, hi)
+        for w in self._pending:
             w.wait()
+        self._pending, self._reduced = [], []
+        self.bw.on_ready = None
 
     def optimizer_step(self):
         s = self.s

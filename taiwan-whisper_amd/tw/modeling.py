@@ -356,6 +356,20 @@ class WhisperForConditionalGeneration:
             return None
         return self.grad[o: o + self.store.numel(n)].view(self.store.segs[n])
 
+    def grad_range(self, prefix):
+        """(lo, hi) of the flat-gradient slice holding every trainable segment named prefix*, or None."""
+        lo, hi = None, None
+        for n in self.store.order:
+            if not n.startswith(prefix):
+                continue
+            o = self.store.offset[n]
+            if o >= self.train_prefix:
+                continue
+            e = o + self.store.numel(n)
+            lo = o if lo is None else min(lo, o)
+            hi = e if hi is None else max(hi, e)
+        return None if lo is None else (lo, hi)
+
     def sync_bf16(self):
         """bf16 mirror := bf16(fp32 master) (autocast's weight cast) for the whole model."""
         if self.store.p32 is not None:
@@ -594,6 +608,14 @@ class Backward:
         self.m = model
         self.dev = model.device
         self._ln_ws = None
+        # on_ready(prefix): called once every gradient of the layer `prefix` (e.g.
+        # "model.decoder.layers.1.") is final, so the DP exchange of that range can start while the
+        # rest of the backward runs
+        self.on_ready = None
+
+    def _layer_done(self, p):
+        if self.on_ready is not None and p.endswith(".self_attn"):
+            self.on_ready(p[: -len("self_attn")])
 
     # dW[N][K] += bf16(g^T x): g [M][N] bf16, x [M][K] bf16
     def dW(self, g, x, dw, M):
@@ -723,6 +745,7 @@ class Backward:
                 self.cross(p, st, dx, enc16, d_enc)
             elif kind == "attn":
                 self.attn(p, st, dx)
+                self._layer_done(p)
             elif kind == "embed":
                 if gE is not None:
                     F.embed_bwd(st["ids"], dx, gE)
@@ -743,6 +766,7 @@ class Backward:
                 self.mlp(p, st, dx)
             elif kind == "attn":
                 self.attn(p, st, dx)
+                self._layer_done(p)
             elif kind == "conv":
                 self.conv(st, dx)
 

@@ -1,8 +1,9 @@
 """Data-parallel semantics on CPU with gloo, world_size 2 (no GPU needed).
 
 1. The product's gradient exchange (`DistillationTrainer.all_reduce_grads`, bucketed async SUM of
-   the flat fp32 gradient with the 1/world factor folded into the loss gradient) equals the DDP
-   mean of per-rank gradients, for bucket sizes that split the buffer unevenly.
+   the flat fp32 gradient with the 1/world factor folded into the loss gradient; per-layer ranges
+   launched early during the backward, the remainder at the end) equals the DDP mean of per-rank
+   gradients, for bucket sizes and early ranges that split the buffer unevenly.
 2. SURVEY.md §8(e) semantics on the oracle step: 2 ranks x half batch with DDP mean == 1 process
    accumulating the two halves with loss / 2 each (per-rank token normalisation kept).
 """
@@ -39,13 +40,23 @@ def _worker_allreduce(rank, world, port, out):
     g = torch.Generator().manual_seed(rank)
     local = torch.randn(n, generator=g)
 
+    import types
+
     class Stub:
         pass
     st = Stub()
     st.s = Stub()
+    st.bw = Stub()
     st.s.grad = local / world            # the trainer folds 1/world into grad_scale
     st.world, st.pg, st.bucket = world, dist.group.WORLD, 3001
+    st._launch = types.MethodType(DistillationTrainer._launch, st)
+    # two "layers" finished during the backward start their exchange early (out of order, uneven
+    # sizes); all_reduce_grads then covers the gaps and waits for everything
+    st._pending, st._reduced = [], []
+    st._launch(6000, 9000)
+    st._launch(100, 2500)
     DistillationTrainer.all_reduce_grads(st)
+    assert st._pending == [] and st._reduced == []
     out[rank] = st.s.grad.clone()
     dist.destroy_process_group()
 

@@ -1,0 +1,101 @@
+"""Data-parallel step on the GPU: 2 ranks sharing cuda:0 over gloo (the 1-GPU box; on 8 GPUs the
+same code runs over RCCL).  The per-layer gradient exchange starts inside the backward
+(Backward.on_ready -> async all-reduce of each finished layer's slice) and the rest follows at the
+end; after one optimizer step both ranks hold identical weights, equal (fp32 summation order aside:
+1e-6 relative on the update) to one process accumulating the two half-batches (DDP mean semantics,
+SURVEY.md §8e)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup():
+    import sys
+    for p in (REPO, os.path.join(REPO, "taiwan-whisper_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from conftest import load_golden
+    from oracle.weights import CONFIGS, make_weights
+    from tw.config import WhisperConfig
+    from tw.modeling import WhisperForConditionalGeneration
+    cfg = CONFIGS["micro"]
+    tc = WhisperConfig(**cfg)
+    mk = lambda seed, dt: WhisperForConditionalGeneration.from_state_dict(
+        tc, {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed).items()}, dtype=dt)
+    g = load_golden("micro_step")
+    return mk, g
+
+
+def _batch(g, lo, hi):
+    return {"input_features": torch.from_numpy(g["feats"][lo:hi]).cuda(),
+            "decoder_input_ids": torch.from_numpy(g["dec"][lo:hi]).cuda(),
+            "labels": torch.from_numpy(g["lab"][lo:hi]).cuda()}
+
+
+def _worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    mk, g = _setup()
+    from tw.distill import DistillationTrainer
+    s, t = mk(1, torch.float32), mk(2, torch.bfloat16)
+    tr = DistillationTrainer(s, t, learning_rate=1e-3, freeze_encoder=False, dp_bucket_mb=1,
+                             process_group=torch.distributed.group.WORLD)
+    launched = []
+    orig = tr._grad_ready
+    tr._grad_ready = lambda p: (launched.append(p), orig(p))
+    B = g["feats"].shape[0]
+    h = B // world
+    tr.train_step(_batch(g, rank * h, (rank + 1) * h))
+    torch.cuda.synchronize()
+    out[rank] = (s.store.p32.cpu().clone(), list(launched))
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_two_ranks_equal_accumulation():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    p0, l0 = out[0]
+    p1, l1 = out[1]
+    assert torch.equal(p0, p1)
+    # every decoder and encoder layer started its exchange inside the backward
+    assert any(p.startswith("model.decoder.layers.") for p in l0) and any(p.startswith("model.encoder.layers.")
+                                                                          for p in l0)
+    # single process, the two halves accumulated (loss / 2 each) = DDP mean of per-rank gradients
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    mk, g = _setup()
+    from tw.distill import DistillationTrainer
+    s, t = mk(1, torch.float32), mk(2, torch.bfloat16)
+    init = s.store.p32.clone()
+    tr = DistillationTrainer(s, t, learning_rate=1e-3, freeze_encoder=False, gradient_accumulation_steps=2)
+    B = g["feats"].shape[0]
+    h = B // world
+    tr.train_step(_batch(g, 0, h))
+    tr.train_step(_batch(g, h, 2 * h))
+    torch.cuda.synchronize()
+    ref = s.store.p32.cpu()
+    d_dp, d_acc = p0 - init.cpu(), ref - init.cpu()
+    rel = float((d_dp - d_acc).norm() / d_acc.norm())
+    assert rel < 1e-3, rel
