@@ -18,6 +18,7 @@
 // 4 consecutive output columns of one row: 8/16-B stores in the epilogue.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -48,6 +49,7 @@ struct GemmP {
   int c_dtype; int flags;
   int tiles_n, tiles_mn, group_m, tiles_total;
   int epi;         // fast epilogue kind chosen on the host (EPI_*), EPI_GENERIC otherwise
+  float* ws;       // skinny split-K: fp32 partials [gridDim.y][M][N] (nullptr: epilogue in place)
 };
 
 __device__ __forceinline__ int xr_mn(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -750,8 +752,12 @@ __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
   const int n0 = blockIdx.x * 16;
   const int li = lane & 15, g = lane >> 4;
   const int nk = (p.K + 31) / 32;                         // 32-deep k-steps
-  const int per = (nk + 3) / 4;
-  const int k_beg = wave * per, k_end = min(nk, k_beg + per);
+  // this workgroup's K chunk (split-K over gridDim.y when the launch has too few workgroups to
+  // keep enough weight loads in flight), then split over the 4 waves
+  const int cper = (nk + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c_beg = (int)blockIdx.y * cper, c_end = min(nk, c_beg + cper);
+  const int per = (c_end - c_beg + 3) / 4;
+  const int k_beg = min(c_end, c_beg + wave * per), k_end = min(c_end, k_beg + per);
   f32x4 acc[MF];
 #pragma unroll
   for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -809,12 +815,26 @@ __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
   __syncthreads();
   for (int e = threadIdx.x; e < MF * 16 * 16; e += 256) {
     const int m = e >> 4, c = e & 15, n = n0 + c;
-    if (m < p.M && n < p.N) epi_element(p, m, n, part[0][m][c] + part[1][m][c] + part[2][m][c] + part[3][m][c]);
+    if (m < p.M && n < p.N) {
+      const float v = part[0][m][c] + part[1][m][c] + part[2][m][c] + part[3][m][c];
+      if (p.ws) p.ws[((int64_t)blockIdx.y * p.M + m) * p.N + n] = v;
+      else epi_element(p, m, n, v);
+    }
   }
 }
 
-void launch_skinny(GemmP p, hipStream_t stream) {
-  const dim3 grid((p.N + 15) / 16);
+// sum of the split-K partials of the skinny kernel (in chunk order) + the full epilogue
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmP p, int S) {
+  const int64_t total = (int64_t)p.M * p.N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = p.ws[i];
+    for (int s = 1; s < S; ++s) v += p.ws[s * total + i];
+    epi_element(p, (int)(i / p.N), (int)(i % p.N), v);
+  }
+}
+
+void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
+  const dim3 grid((p.N + 15) / 16, S);
   const int mf = (p.M + 15) / 16;
   switch (mf) {
     case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, stream, p); break;
@@ -873,7 +893,7 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
 // workspace, then one pass sums the chunks in order and applies the epilogue
 //     C = [C +] round?(alpha * sum_s ws[s])
 // (bf16 rounding point of the autocast product as in the unsplit kernel; the fp32 sum over K is
-// regrouped by chunk).  Workspace: lazily grown per (device, stream), never freed.
+// regrouped by chunk).  Workspace: splitk_workspace (per device, never freed).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t split_stride,
                                                             float* __restrict__ C, int64_t ldc, int M, int N,
@@ -894,30 +914,30 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-struct SplitWs {
-  int dev; hipStream_t stream; void* ptr; size_t bytes;
-};
-
+// Split-K workspace: one block per device, grown (never freed: a captured HIP graph may hold the
+// pointer of an older block, so old blocks are kept) outside stream capture only.  GEMMs of one
+// device are issued from one stream at a time (the trainer's and the decoder's current stream).
 void* splitk_workspace(hipStream_t stream, size_t bytes) {
   static std::mutex mu;
-  static std::vector<SplitWs> table;
+  static std::vector<std::pair<int, std::pair<void*, size_t>>> cur;   // device -> (ptr, bytes)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cap);
   std::lock_guard<std::mutex> lock(mu);
-  for (auto& e : table)
-    if (e.dev == dev && e.stream == stream) {
-      if (e.bytes >= bytes) return e.ptr;
-      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;    // the old block may still be read
-      (void)hipFree(e.ptr);
-      e.ptr = nullptr;
-      e.bytes = 0;
-      if (hipMalloc(&e.ptr, bytes) != hipSuccess) return nullptr;
-      e.bytes = bytes;
-      return e.ptr;
+  for (auto& e : cur)
+    if (e.first == dev) {
+      if (e.second.second >= bytes) return e.second.first;
+      if (cap != hipStreamCaptureStatusNone) return nullptr;
+      void* ptr = nullptr;
+      if (hipMalloc(&ptr, bytes) != hipSuccess) return nullptr;
+      e.second = {ptr, bytes};                                           // the old block stays allocated
+      return ptr;
     }
+  if (cap != hipStreamCaptureStatusNone) return nullptr;
   void* ptr = nullptr;
   if (hipMalloc(&ptr, bytes) != hipSuccess) return nullptr;
-  table.push_back({dev, stream, ptr, bytes});
+  cur.push_back({dev, {ptr, bytes}});
   return ptr;
 }
 
@@ -968,6 +988,7 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   p.sA = sA; p.sB = sB; p.sC = sC; p.alpha = alpha; p.bias = (const bf16*)bias;
   p.res = res; p.ldr = ldr; p.sR = sR; p.res_dtype = res_dtype; p.res_mod = res_mod;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux; p.c_dtype = c_dtype; p.flags = flags;
+  p.ws = nullptr;
   static const int env_group = [] {
     const char* e = getenv("TW_GEMM_GROUP_M");   // A/B sweeps only (tools/bench_gemm.py)
     return e ? atoi(e) : 0;
@@ -993,17 +1014,30 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && (N <= 4096 || (M <= 64 && N <= 8192)) &&
                       !(flags & (256 | 512 | 1024 | 2048));
   if (skinny && ((uintptr_t)A & 15) == 0) {
-    launch_skinny(p, stream);                         // decode-step GEMMs: stream W once
+    // decode-step GEMMs: stream W once.  With fewer than 512 workgroups the K range is also split
+    // over workgroups (chunks of >= 4 k-steps) into fp32 partials, reduced with the epilogue.
+    p.ws = nullptr;
+    const int nwg = (N + 15) / 16, nk = (K + 31) / 32;
+    int S = std::min((512 + nwg - 1) / nwg, nk / 4);
+    if (flags & 16384) S = 1;
+    void* ws = S > 1 ? splitk_workspace(stream, (size_t)S * M * N * sizeof(float)) : nullptr;
+    if (ws) {
+      p.ws = (float*)ws;
+      launch_skinny(p, stream, S);
+      TW_CHECK_LAUNCH();
+      const int64_t total = (int64_t)M * N;
+      hipLaunchKernelGGL(skinny_reduce_kernel, dim3((int)std::min<int64_t>((total + 255) / 256, 2048)), dim3(256), 0,
+                         stream, p, S);
+    } else {
+      launch_skinny(p, stream);
+    }
     TW_CHECK_LAUNCH();
     return TW_OK;
   }
   if (!(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
     const int S = splitk_factor(p, batch, a_trans, b_trans);
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(stream, &cap);
     const size_t bytes = (size_t)S * M * N * sizeof(float);
-    void* ws = (S > 0 && cap == hipStreamCaptureStatusNone && bytes <= ((size_t)1 << 30))
-                   ? splitk_workspace(stream, bytes) : nullptr;
+    void* ws = (S > 0 && bytes <= ((size_t)1 << 30)) ? splitk_workspace(stream, bytes) : nullptr;
     if (ws) {
       GemmP q = p;
       const int Kc = K / S;
