@@ -134,7 +134,30 @@ struct SelP {
   int begin_col;
   const uint32_t* ctl;        // nullable: [0] = bits of 1/T (0: greedy), [1], [2] = seed lo, hi
   float* sum_logp;            // nullable: += log-prob of the chosen token while the row is live
+  int vec;                    // rows 16-B aligned and padded to a multiple of 8 ids: 16-B loads
 };
+
+// f(v, x, suppressed, begin_suppressed) over this thread's ids of a logits row: chunks of 8
+// consecutive ids (one 16-B load, one word of each mask), chunk c = tid, tid + 256, ...
+template <class F>
+__device__ __forceinline__ void for_row(const SelP& p, const bf16* row, F&& f) {
+  for (int v0 = (int)threadIdx.x * 8; v0 < p.V; v0 += 256 * 8) {
+    float xs[8];
+    if (p.vec) {
+      const bf16x8 t = *(const bf16x8*)(row + v0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xs[j] = bf2f(t[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xs[j] = v0 + j < p.V ? bf2f(row[v0 + j]) : -INFINITY;
+    }
+    const uint32_t ws = p.suppress ? p.suppress[v0 >> 5] >> (v0 & 31) : 0u;   // 8 ids never straddle a word
+    const uint32_t wb = p.begin ? p.begin[v0 >> 5] >> (v0 & 31) : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (v0 + j < p.V) f(v0 + j, xs[j], ((ws >> j) & 1u) != 0u, ((wb >> j) & 1u) != 0u);
+  }
+}
 
 // (max, sum exp(x - max)) pairs: running logsumexp
 __device__ __forceinline__ void lse_add(float& m, float& s, float x) {
@@ -207,9 +230,8 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
   const bf16* row = p.logits + b * p.ld;
   float best = -INFINITY, sbest = -INFINITY, m = -INFINITY, se = 0.f;
   int besti = 0x7fffffff, sbesti = 0x7fffffff;
-  for (int v = tid; v < p.V; v += 256) {
-    float x = bf2f(row[v]);
-    if (bit(p.suppress, v) || (p.apply_begin && bit(p.begin, v))) x = -INFINITY;
+  for_row(p, row, [&](int v, float x, bool sup, bool beg) {
+    if (sup || (p.apply_begin && beg)) x = -INFINITY;
     if (x > best || (x == best && v < besti)) { best = x; besti = v; }
     if (x > -INFINITY) {
       lse_add(m, se, x);
@@ -218,7 +240,7 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
         if (g > sbest || (g == sbest && v < sbesti)) { sbest = g; sbesti = v; }
       }
     }
-  }
+  });
   block_argmax(best, besti, sv, si, 0);
   if (sample) block_argmax(sbest, sbesti, sv, si, 1);
   if (p.sum_logp) block_lse(m, se, sv, 2);
@@ -274,8 +296,8 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   const int ts_hi = (first && q.max_initial >= 0) ? q.ts_begin + q.max_initial : 0x7fffffff;
   const bf16* row = p.logits + b * p.ld;
   // eligibility of id v before the "timestamp mass wins" rule
-  auto masked = [&](int v) -> bool {
-    bool m = bit(p.suppress, v) || (first && bit(p.begin, v)) || v == q.no_ts;
+  auto masked = [&](int v, bool sup, bool beg) -> bool {
+    bool m = sup || (first && beg) || v == q.no_ts;
     if (v >= q.ts_begin) {
       if (last_ts && pen_ts) m = true;
       if (v < lim || v > ts_hi) m = true;
@@ -287,9 +309,8 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   float bt = -INFINITY, bs = -INFINITY, se = 0.f;        // best text, best timestamp, sum exp(ts - bs)
   float tm = -INFINITY, tse = 0.f;                       // text logsumexp (for the log-prob)
   int it = 0x7fffffff, is = 0x7fffffff;
-  for (int v = tid; v < p.V; v += 256) {
-    const float x = bf2f(row[v]);
-    if (masked(v) || !(x > -INFINITY)) continue;
+  for_row(p, row, [&](int v, float x, bool sup, bool beg) {
+    if (masked(v, sup, beg) || !(x > -INFINITY)) return;
     if (v >= q.ts_begin) {
       if (x > bs) { se = se * __expf(bs - x) + 1.f; bs = x; is = v; }
       else { se += __expf(x - bs); if (x == bs && v < is) is = v; }
@@ -297,7 +318,7 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
       if (x > bt || (x == bt && v < it)) { bt = x; it = v; }
       lse_add(tm, tse, x);
     }
-  }
+  });
   // wave reduction: text (max, argmin idx), timestamps (max, argmin idx, rescaled sum)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -339,12 +360,11 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   int spick = 0x7fffffff;
   if (sample) {                                          // second pass: Gumbel-max over the processed row
     float sb = -INFINITY;
-    for (int v = tid; v < p.V; v += 256) {
-      const float x = bf2f(row[v]);
-      if (masked(v) || !(x > -INFINITY) || (mask_text && v < q.ts_begin)) continue;
+    for_row(p, row, [&](int v, float x, bool sup, bool beg) {
+      if (masked(v, sup, beg) || !(x > -INFINITY) || (mask_text && v < q.ts_begin)) return;
       const float g = x * inv_t + gumbel(seed, b, p.col, v);
       if (g > sb || (g == sb && v < spick)) { sb = g; spick = v; }
-    }
+    });
     block_argmax(sb, spick, sx, sxi, 2);
   }
   if (tid == 0) {
@@ -416,6 +436,11 @@ __global__ void step_advance_kernel(int* t_dev, int by) {
   if (threadIdx.x == 0) *t_dev += by;
 }
 
+// 16-B row loads when every row starts 16-B aligned and has room for the last 8-id chunk
+int sel_vec(const void* logits, int64_t ld, int V) {
+  return ((uintptr_t)logits % 16 == 0 && ld % 8 == 0 && ld >= (int64_t)((V + 7) / 8) * 8) ? 1 : 0;
+}
+
 }  // namespace
 
 extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
@@ -429,7 +454,7 @@ extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V,
   q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
   q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
-  q.s.ctl = nullptr; q.s.sum_logp = nullptr;
+  q.s.ctl = nullptr; q.s.sum_logp = nullptr; q.s.vec = sel_vec(logits, ld, V);
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
   hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
   TW_CHECK_LAUNCH();
@@ -449,7 +474,7 @@ extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int B, int V,
   q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
   q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
-  q.s.ctl = ctl; q.s.sum_logp = sum_logp;
+  q.s.ctl = ctl; q.s.sum_logp = sum_logp; q.s.vec = sel_vec(logits, ld, V);
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
   hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
   TW_CHECK_LAUNCH();
@@ -523,7 +548,7 @@ extern "C" int tw_greedy_select(const void* logits, int64_t ld, int B, int V, co
   p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
-  p.ctl = nullptr; p.sum_logp = nullptr;
+  p.ctl = nullptr; p.sum_logp = nullptr; p.vec = sel_vec(logits, ld, V);
   hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
@@ -541,7 +566,7 @@ extern "C" int tw_select_sample(const void* logits, int64_t ld, int B, int V, co
   p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
-  p.ctl = ctl; p.sum_logp = sum_logp;
+  p.ctl = ctl; p.sum_logp = sum_logp; p.vec = sel_vec(logits, ld, V);
   hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;

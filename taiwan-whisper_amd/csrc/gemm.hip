@@ -1014,12 +1014,13 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && (N <= 4096 || (M <= 64 && N <= 8192)) &&
                       !(flags & (256 | 512 | 1024 | 2048));
   if (skinny && ((uintptr_t)A & 15) == 0) {
-    // decode-step GEMMs: stream W once.  With fewer than 512 workgroups the K range is also split
-    // over workgroups (chunks of >= 4 k-steps) into fp32 partials, reduced with the epilogue.
+    // decode-step GEMMs: stream W once.  With fewer than 512 workgroups and M > 32 the K range is
+    // also split over workgroups (chunks of >= 4 k-steps) into fp32 partials, reduced with the
+    // epilogue (c4 batch 64 / 128: -3 / -4 % per step; at batch 1 the extra launch loses 9 %).
     p.ws = nullptr;
     const int nwg = (N + 15) / 16, nk = (K + 31) / 32;
     int S = std::min((512 + nwg - 1) / nwg, nk / 4);
-    if (flags & 16384) S = 1;
+    if ((flags & 16384) || M <= 32) S = 1;          // small batches: the reduce launch costs more than it saves
     void* ws = S > 1 ? splitk_workspace(stream, (size_t)S * M * N * sizeof(float)) : nullptr;
     if (ws) {
       p.ws = (float*)ws;
