@@ -69,6 +69,58 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
   }
 }
 
+// bf16 -> bf16 rows with D % 256 == 0 (the teacher's bf16 residual stream): a half-wave per row
+// (8 rows per 256-thread block), NCH chunks of 8 bf16 per lane as 16-B loads / stores, statistics
+// reduced over the 32 lanes of the half (same two-pass mean / variance as ln_fwd_kernel).
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, bf16* __restrict__ y,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          int rows, int D, float eps) {
+  const int lane = lane_id(), hl = lane & 31;
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool ok = row < rows;
+  const int64_t base = (int64_t)(ok ? row : 0) * D;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 32 + hl) * 8;
+    const bf16x8 t = ok ? *(const bf16x8*)(x + base + e) : bf16x8{};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { v[c][q] = bf2f(t[q]); s += v[c][q]; }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { const float d = v[c][q] - mean; ss += d * d; }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float rstd = rsqrtf(ss / D + eps);
+  if (!ok) return;
+  if (hl == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 32 + hl) * 8;
+    const f32x4 w0 = *(const f32x4*)(w + e), w1 = *(const f32x4*)(w + e + 4);
+    const f32x4 b0 = *(const f32x4*)(b + e), b1 = *(const f32x4*)(b + e + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[q] = f2bf((v[c][q] - mean) * rstd * w0[q] + b0[q]);
+      o[q + 4] = f2bf((v[c][q + 4] - mean) * rstd * w1[q] + b1[q]);
+    }
+    *(bf16x8*)(y + base + e) = o;
+  }
+}
+
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)); dx accumulated into dx_out (fp32).
 // Per-block partial dw/db written to partial[blockIdx.x][2][D] for a column reduction.
 template <int VEC, int MAXJ>
@@ -163,7 +215,22 @@ extern "C" int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, cons
   if (rows <= 0) return TW_OK;
   if (D % 64 || D > 1280) return TW_EUNSUPPORTED;
   dim3 grid((rows + WPB - 1) / WPB), block(64 * WPB);
-  if (D % 256 == 0)
+  const bool a16 = (((uintptr_t)x | (uintptr_t)y | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
+  if (x_dtype == TW_BF16 && y_dtype == TW_BF16 && D % 256 == 0 && a16) {
+    const dim3 g2((rows + 2 * WPB - 1) / (2 * WPB));
+    switch (D / 256) {
+      case 1: hipLaunchKernelGGL(ln_fwd_bf16_kernel<1>, g2, block, 0, stream, (const bf16*)x, w, b, (bf16*)y, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      case 2: hipLaunchKernelGGL(ln_fwd_bf16_kernel<2>, g2, block, 0, stream, (const bf16*)x, w, b, (bf16*)y, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      case 3: hipLaunchKernelGGL(ln_fwd_bf16_kernel<3>, g2, block, 0, stream, (const bf16*)x, w, b, (bf16*)y, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      case 4: hipLaunchKernelGGL(ln_fwd_bf16_kernel<4>, g2, block, 0, stream, (const bf16*)x, w, b, (bf16*)y, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      default: hipLaunchKernelGGL(ln_fwd_bf16_kernel<5>, g2, block, 0, stream, (const bf16*)x, w, b, (bf16*)y, mean_out,
+                                  rstd_out, rows, D, eps); break;
+    }
+  } else if (D % 256 == 0)
     hipLaunchKernelGGL((ln_fwd_kernel<4, 5>), grid, block, 0, stream, x, x_dtype, w, b, y, y_dtype, mean_out,
                        rstd_out, rows, D, eps);
   else
