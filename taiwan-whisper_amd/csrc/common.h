@@ -48,9 +48,43 @@ __device__ __forceinline__ float erf_fast(float z) {
   const float e = __builtin_amdgcn_exp2f(-(a * a) * 1.44269504088896341f);
   return copysignf(fmaf(-q, e, 1.0f), z);
 }
-__device__ __forceinline__ float gelu_erf(float x) {   // GELU (HF ACT2FN["gelu"], erf form)
-  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f));
+// Two GELUs at once in the Phi form, gelu(x) = x * Phi(x) with Phi(x) = 1 - h (x >= 0), h (x < 0),
+// h = erfc(|x|/sqrt2) / 2 = (t * P(t) / 2) * exp(-x^2/2) (the A&S 7.1.26 polynomial as above,
+// coefficients pre-halved): the FMA/MUL chain runs as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32,
+// two lanes' worth per instruction), only rcp / exp2 / the select stay scalar.  Same error
+// bound as gelu_erf; for x < 0 it avoids the 1 - (1 - small) cancellation.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 ax = {__builtin_fabsf(x.x), __builtin_fabsf(x.y)};
+  const f32x2 a = ax * 0.70710678118654752440f;
+  const f32x2 d = a * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 q = t * 0.5307027145f + -0.7265760135f;
+  q = q * t + 0.7107068705f;
+  q = q * t + -0.142248368f;
+  q = q * t + 0.127414796f;
+  q = q * t;
+  const f32x2 w = (x * x) * -0.72134752044448170f;          // -x^2/2 * log2(e)
+  const f32x2 e = {__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+  const f32x2 h = q * e;
+  const f32x2 g = 1.0f - h;
+  const f32x2 phi = {x.x >= 0.f ? g.x : h.x, x.y >= 0.f ? g.y : h.y};
+  return x * phi;
 }
+// GELU (HF ACT2FN["gelu"], erf form), one value: the operation sequence of gelu_erf2, so every
+// epilogue (packed fast path, generic, per-element) rounds identically
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float a = __builtin_fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(a * 0.3275911f + 1.0f);
+  float q = t * 0.5307027145f + -0.7265760135f;
+  q = q * t + 0.7107068705f;
+  q = q * t + -0.142248368f;
+  q = q * t + 0.127414796f;
+  q = q * t;
+  const float h = q * __builtin_amdgcn_exp2f((x * x) * -0.72134752044448170f);
+  return x * (x >= 0.f ? 1.0f - h : h);
+}
+
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752440f));
   const float pdf = 0.39894228040143267794f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);

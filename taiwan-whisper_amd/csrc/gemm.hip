@@ -16,419 +16,12 @@
 // s ^ ((r & 3) | ((r >> 3) & 1) << 2), read with ds_read_b64_tr_b16 (conflict-free).
 // The MFMA is issued with operands swapped (Bfrag, Afrag) so each lane ends up holding
 // 4 consecutive output columns of one row: 8/16-B stores in the epilogue.
-#include "common.h"
+#include "gemm_impl.h"
 
-#include <algorithm>
-#include <cstdlib>
-#include <mutex>
-#include <vector>
 
 namespace {
 
-constexpr int BK = 64;
-
-enum {
-  F_BIAS = 1,      // v += bias[n]            (bias bf16, autocast casts it)
-  F_ROUND = 2,     // v = bf16(v)             (autocast Linear output)
-  F_GELU = 4,      // [aux = v]; v = bf16(gelu(v))
-  F_RES = 8,       // v = res[m % res_mod][n] + v
-  F_ACCUM = 16,    // v += C_old
-  F_AUX_OUT = 32,  // store pre-activation to aux (with F_GELU)
-  F_DGELU = 64,    // v = bf16(v * gelu'(aux[m][n]))  (gelu backward, aux = pre-activation)
-};
-
-struct GemmP {
-  const bf16* A; const bf16* B; void* C;
-  int64_t lda, ldb, ldc;
-  int M, N, K;
-  int64_t sA, sB, sC;
-  float alpha;
-  const bf16* bias;
-  const void* res; int64_t ldr; int64_t sR; int res_dtype; int res_mod;
-  bf16* aux; int64_t ldaux; int64_t sAux;
-  int c_dtype; int flags;
-  int tiles_n, tiles_mn, group_m, tiles_total;
-  int epi;         // fast epilogue kind chosen on the host (EPI_*), EPI_GENERIC otherwise
-  float* ws;       // skinny split-K: fp32 partials [gridDim.y][M][N] (nullptr: epilogue in place)
-};
-
-__device__ __forceinline__ int xr_mn(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
-
-// K-major tile [R rows][64 k] -> LDS, 128-B rows, 16-B chunk c of row r at c ^ (r & 7).
-// R/8 pieces of 1 KiB (8 rows each), NW waves.
-template <int R, int NW>
-__device__ __forceinline__ void stage_k(const bf16* base, int64_t ld, int rows_left, int k_left, char* lds, int wave,
-                                        int lane) {
-  const auto rs = make_rsrc(base);
-#pragma unroll
-  for (int i = 0; i < R / 8 / NW; ++i) {
-    const int pce = wave + NW * i;
-    const int r = pce * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (r & 7);
-    const bool ok = (r < rows_left) && (c * 8 < k_left);
-    const uint32_t off = ok ? (uint32_t)(((int64_t)r * ld + c * 8) * 2) : TW_OOB;
-    buf_load_lds16(rs, lds + pce * 1024, off);
-  }
-}
-
-// MN-major tile [64 k-rows][R cols] -> LDS, 2R-byte k-rows, 32-B slot s of k-row r at s ^ xr_mn(r).
-template <int R, int NW>
-__device__ __forceinline__ void stage_mn(const bf16* base, int64_t ld, int cols_left, int k_left, char* lds, int wave,
-                                         int lane) {
-  const auto rs = make_rsrc(base);
-  constexpr int LPR = R / 8;          // lanes (16-B chunks) per k-row
-  constexpr int RPP = 64 / LPR;       // k-rows per 1-KiB piece
-#pragma unroll
-  for (int i = 0; i < R / 8 / NW; ++i) {
-    const int pce = wave + NW * i;
-    const int kr = pce * RPP + lane / LPR;
-    const int pc = lane % LPR;
-    const int s = (pc >> 1) ^ xr_mn(kr);
-    const int col = s * 16 + (pc & 1) * 8;
-    const bool ok = (kr < k_left) && (col < cols_left);
-    const uint32_t off = ok ? (uint32_t)(((int64_t)kr * ld + col) * 2) : TW_OOB;
-    buf_load_lds16(rs, lds + pce * 1024, off);
-  }
-}
-
-__device__ __forceinline__ bf16x8 frag_k(const char* tile, int rbase, int kk, int lane) {
-  const int r = rbase + (lane & 15);
-  const int c = kk * 4 + (lane >> 4);
-  return *(const bf16x8*)(tile + r * 128 + ((c ^ (r & 7)) << 4));
-}
-
-template <int R>
-__device__ __forceinline__ bf16x8 frag_mn(const char* tile, int cbase, int kk, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int col = cbase + 4 * (i & 3);
-  const int slot = col >> 4, inoff = (col & 15) * 2;
-  const int kr0 = kk * 32 + 8 * g + (i >> 2);
-  const int kr1 = kr0 + 4;
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const char* a0 = tile + kr0 * (2 * R) + ((slot ^ xr_mn(kr0)) << 5) + inoff;
-  const char* a1 = tile + kr1 * (2 * R) + ((slot ^ xr_mn(kr1)) << 5) + inoff;
-  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
-  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a1);
-  s16x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// Block tile BMxBN, waves WMxWN (each (BM/WM)x(BN/WN)), two LDS stages, one barrier per K-step.
-// blockIdx.x enumerates (m-tile, n-tile) pairs remapped so that consecutive tiles of one m-row
-// share an XCD (L2 reuse of the A panel; blocks b and b+8 share an XCD).
-template <int N>
-__device__ __forceinline__ void wait_vm_lgkm0() {   // s_waitcnt vmcnt(N) lgkmcnt(0), N compile-time
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-  else static_assert(N < 0, "add the vmcnt immediate");
-}
-
-// Linear tile id -> (m-tile, n-tile), grouped: runs of group_m m-tiles are walked n-tile by
-// n-tile, so the ~32 tiles one XCD holds at a time share group_m A panels and 32/group_m B
-// panels in its L2 (group_m = 1: plain row-major).
-__device__ __forceinline__ void tile_coords(int tid, const GemmP& p, int& mt, int& nt) {
-  const int tiles_m = p.tiles_mn / p.tiles_n;
-  const int per_group = p.group_m * p.tiles_n;
-  const int g = tid / per_group, first = g * p.group_m;
-  const int gm = min(p.group_m, tiles_m - first);
-  const int r = tid - g * per_group;
-  mt = first + r % gm;
-  nt = r / gm;
-}
-
-// Generic epilogue (any flag combination, ragged edges): lane holds C[m][n..n+3] of each 16x16
-// fragment (swapped-operand MFMA layout).
-template <int BM, int BN, int WM, int WN>
-__device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                         int n0, int wm, int wn, int lane, int bz) {
-  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  const int g = lane >> 4, li = lane & 15;
-  const int flags = p.flags;
-  char* C = (char*)p.C;
-  const bool full_tile = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 3) == 0) &&
-                         (!(flags & F_RES) || ((p.ldr & 3) == 0 && p.res_mod == 0)) &&
-                         (!(flags & (F_AUX_OUT | F_DGELU)) || (p.ldaux & 3) == 0);
-  if (full_tile) {
-    // fast path: no bounds checks, vector loads/stores, bias hoisted, loads of one fragment
-    // row issued before any of its stores (C may alias res for in-place residual updates)
-    float bv[FN][4];
-#pragma unroll
-    for (int ni = 0; ni < FN; ++ni) {
-      if (flags & F_BIAS) {
-        const bf16x4 t = *(const bf16x4*)(p.bias + n0 + wn * (BN / WN) + ni * 16 + 4 * g);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[ni][r] = bf2f(t[r]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int mi = 0; mi < FM; ++mi) {
-      const int m = m0 + wm * (BM / WM) + mi * 16 + li;
-      const int nb = n0 + wn * (BN / WN) + 4 * g;
-      float ex[FN][4];     // residual / old-C / aux operand, loaded up front
-      if (flags & (F_RES | F_ACCUM | F_DGELU)) {
-#pragma unroll
-        for (int ni = 0; ni < FN; ++ni) {
-          const int n = nb + ni * 16;
-          if (flags & F_DGELU) {
-            const bf16x4 t = *(const bf16x4*)(p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ex[ni][r] = bf2f(t[r]);
-          } else {
-            const bool res = flags & F_RES;
-            const void* src = res ? p.res : (const void*)C;
-            const int dt = res ? p.res_dtype : p.c_dtype;
-            const int64_t o = res ? bz * p.sR + (int64_t)m * p.ldr + n : bz * p.sC + (int64_t)m * p.ldc + n;
-            if (dt == TW_BF16) {
-              const bf16x4 t = *(const bf16x4*)((const bf16*)src + o);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) ex[ni][r] = bf2f(t[r]);
-            } else {
-              const f32x4 t = *(const f32x4*)((const float*)src + o);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) ex[ni][r] = t[r];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int ni = 0; ni < FN; ++ni) {
-        const int n = nb + ni * 16;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = p.alpha * acc[mi][ni][r] + bv[ni][r];
-          if (flags & F_ROUND) v[r] = rbf(v[r]);
-          if (flags & F_DGELU) v[r] = rbf(v[r] * gelu_erf_grad(ex[ni][r]));
-        }
-        if (flags & F_GELU) {
-          if (flags & F_AUX_OUT)
-            *(bf16x4*)(p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n) =
-                bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_erf(v[r]));
-        }
-        if (flags & (F_RES | F_ACCUM)) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += ex[ni][r];
-        }
-        const int64_t co = bz * p.sC + (int64_t)m * p.ldc + n;
-        if (p.c_dtype == TW_BF16) *(bf16x4*)((bf16*)C + co) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        else *(f32x4*)((float*)C + co) = f32x4{v[0], v[1], v[2], v[3]};
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int mi = 0; mi < FM; ++mi) {
-    const int m = m0 + wm * (BM / WM) + mi * 16 + li;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int ni = 0; ni < FN; ++ni) {
-      const int n = n0 + wn * (BN / WN) + ni * 16 + 4 * g;
-      if (n >= p.N) continue;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[mi][ni][r];
-      const bool full = (n + 3 < p.N);
-      const int nv = full ? 4 : (p.N - n);
-      if (flags & F_BIAS) {
-        for (int r = 0; r < nv; ++r) v[r] += bf2f(p.bias[n + r]);
-      }
-      if (flags & F_ROUND) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = rbf(v[r]);
-      }
-      if (flags & F_DGELU) {
-        const bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
-        for (int r = 0; r < nv; ++r) v[r] = rbf(v[r] * gelu_erf_grad(bf2f(ax[r])));
-      }
-      if (flags & F_GELU) {
-        if (flags & F_AUX_OUT) {
-          bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
-          for (int r = 0; r < nv; ++r) ax[r] = f2bf(v[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_erf(v[r]));
-      }
-      if (flags & F_RES) {
-        const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
-        const int64_t ro = bz * p.sR + (int64_t)mr * p.ldr + n;
-        for (int r = 0; r < nv; ++r) v[r] += ld_as_f32(p.res, p.res_dtype, ro + r);
-      }
-      const int64_t co = bz * p.sC + (int64_t)m * p.ldc + n;
-      if (flags & F_ACCUM) {
-        for (int r = 0; r < nv; ++r) v[r] += ld_as_f32(C, p.c_dtype, co + r);
-      }
-      if (p.c_dtype == TW_BF16) {
-        bf16* cp = (bf16*)C + co;
-        if (full && ((co & 3) == 0)) {
-          *(bf16x4*)cp = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        } else {
-          for (int r = 0; r < nv; ++r) cp[r] = f2bf(v[r]);
-        }
-      } else {
-        float* cp = (float*)C + co;
-        if (full && ((co & 3) == 0)) {
-          *(f32x4*)cp = f32x4{v[0], v[1], v[2], v[3]};
-        } else {
-          for (int r = 0; r < nv; ++r) cp[r] = v[r];
-        }
-      }
-    }
-  }
-}
-
-
-// ---------------------------------------------------------------------------------------------
-// Specialised full-tile epilogues for the step's hot flag combinations (chosen on the host, so
-// the per-element code carries no flag branches).  bf16 tiles are written 16 B per lane: the
-// fragments (ni, ni+1) of one row block are exchanged with v_permlane16_swap, after which lane
-// (li, g) holds 8 consecutive columns at  16*ni + (g&1)*16 + (g>>1)*8  (64 contiguous bytes per
-// row per store instruction instead of 32).  The same exchange maps a 16-B residual load back
-// to fragment order (the swap is an involution), so each lane reads and writes the same bytes
-// (in-place residual updates stay race-free).
-// ---------------------------------------------------------------------------------------------
-enum { EPI_GENERIC = 0, EPI_STORE_BF16, EPI_STORE_F32, EPI_GELU, EPI_GELU_AUX, EPI_RES_BF16, EPI_RES_F32 };
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t pack2(float a, float b) {
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  return __builtin_bit_cast(uint32_t, bf16x2{f2bf(a), f2bf(b)});
-}
-__device__ __forceinline__ float lo_bf(uint32_t u) { return __builtin_bit_cast(float, u << 16); }
-__device__ __forceinline__ float hi_bf(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
-
-// fragments X (ni) and Y (ni+1), 4 floats each -> this lane's 16 B of the pair (swapped layout)
-__device__ __forceinline__ u32x4 pair_to_u4(const float (&x)[4], const float (&y)[4]) {
-  const uint32_t x0 = pack2(x[0], x[1]), x1 = pack2(x[2], x[3]);
-  const uint32_t y0 = pack2(y[0], y[1]), y1 = pack2(y[2], y[3]);
-  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-  return u32x4{s0[0], s1[0], s0[1], s1[1]};
-}
-// inverse: this lane's 16 B of the pair (swapped layout) -> fragments X, Y as floats
-__device__ __forceinline__ void u4_to_pair(u32x4 r, float (&x)[4], float (&y)[4]) {
-  const auto s0 = __builtin_amdgcn_permlane16_swap(r[0], r[2], false, false);
-  const auto s1 = __builtin_amdgcn_permlane16_swap(r[1], r[3], false, false);
-  x[0] = lo_bf(s0[0]); x[1] = hi_bf(s0[0]); x[2] = lo_bf(s1[0]); x[3] = hi_bf(s1[0]);
-  y[0] = lo_bf(s0[1]); y[1] = hi_bf(s0[1]); y[2] = lo_bf(s1[1]); y[3] = hi_bf(s1[1]);
-}
-
-template <int BM, int BN, int WM, int WN, int KIND>
-__device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                              int n0, int wm, int wn, int lane, int bz) {
-  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  static_assert(FN % 2 == 0, "fragment pairs");
-  const int g = lane >> 4, li = lane & 15;
-  const int cw = n0 + wn * (BN / WN);                 // wave's first column
-  const int sw = (g & 1) * 16 + (g >> 1) * 8;        // this lane's column in a swapped pair
-  const bool rnd = p.flags & F_ROUND;
-  float bv[FN][4];
-#pragma unroll
-  for (int ni = 0; ni < FN; ++ni) {
-    if (p.flags & F_BIAS) {
-      const bf16x4 t = *(const bf16x4*)(p.bias + cw + ni * 16 + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[ni][r] = bf2f(t[r]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
-    }
-  }
-#pragma unroll
-  for (int mi = 0; mi < FM; ++mi) {
-    const int64_t m = m0 + wm * (BM / WM) + mi * 16 + li;
-    // residual operand of the whole row block, loaded before any store of it
-    u32x4 rb[FN / 2];
-    f32x4 rf[FN];
-    if constexpr (KIND == EPI_RES_BF16) {
-      const bf16* rrow = (const bf16*)p.res + bz * p.sR + m * p.ldr + cw;
-#pragma unroll
-      for (int np = 0; np < FN / 2; ++np) rb[np] = *(const u32x4*)(rrow + np * 32 + sw);
-    }
-    if constexpr (KIND == EPI_RES_F32) {
-      const float* rrow = (const float*)p.res + bz * p.sR + m * p.ldr + cw;
-#pragma unroll
-      for (int ni = 0; ni < FN; ++ni) rf[ni] = *(const f32x4*)(rrow + ni * 16 + 4 * g);
-    }
-#pragma unroll
-    for (int np = 0; np < FN / 2; ++np) {
-      float v[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[h][r] = p.alpha * acc[mi][2 * np + h][r] + bv[2 * np + h][r];
-      if constexpr (KIND == EPI_STORE_BF16) {
-        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
-      } else if constexpr (KIND == EPI_STORE_F32) {
-        float* crow = (float*)p.C + bz * p.sC + m * p.ldc + cw;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f32x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = rnd ? rbf(v[h][r]) : v[h][r];
-          *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
-        }
-      } else if constexpr (KIND == EPI_GELU || KIND == EPI_GELU_AUX) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[h][r] = rbf(v[h][r]);     // autocast: Linear output is bf16
-        if constexpr (KIND == EPI_GELU_AUX) {
-          bf16* arow = p.aux + bz * p.sAux + m * p.ldaux + cw;
-          *(u32x4*)(arow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[h][r] = gelu_erf(v[h][r]);
-        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
-      } else if constexpr (KIND == EPI_RES_BF16) {
-        float x[4], y[4];
-        u4_to_pair(rb[np], x, y);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[0][r] = (rnd ? rbf(v[0][r]) : v[0][r]) + x[r];
-          v[1][r] = (rnd ? rbf(v[1][r]) : v[1][r]) + y[r];
-        }
-        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
-      } else {   // EPI_RES_F32
-        float* crow = (float*)p.C + bz * p.sC + m * p.ldc + cw;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f32x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (rnd ? rbf(v[h][r]) : v[h][r]) + rf[2 * np + h][r];
-          *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
-        }
-      }
-    }
-  }
-}
-
-template <int BM, int BN, int WM, int WN>
-__device__ __forceinline__ void epilogue(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                         int n0, int wm, int wn, int lane, int bz) {
-  const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
-  const int k = full ? p.epi : EPI_GENERIC;
-  if (k == EPI_STORE_BF16) epilogue_fast<BM, BN, WM, WN, EPI_STORE_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_STORE_F32) epilogue_fast<BM, BN, WM, WN, EPI_STORE_F32>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_GELU) epilogue_fast<BM, BN, WM, WN, EPI_GELU>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_GELU_AUX) epilogue_fast<BM, BN, WM, WN, EPI_GELU_AUX>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_RES_BF16) epilogue_fast<BM, BN, WM, WN, EPI_RES_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_RES_F32) epilogue_fast<BM, BN, WM, WN, EPI_RES_F32>(p, acc, m0, n0, wm, wn, lane, bz);
-  else epilogue_generic<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
-}
+using namespace twg;
 
 // STAGES-deep LDS ring, prefetch distance STAGES-1; waits are counted (vmcnt = loads of the
 // stages allowed to stay in flight) and the barrier is a raw s_barrier, so in-flight LDS-DMA
@@ -578,20 +171,11 @@ __device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_
 // contiguous chunk.  The K-tile stream is continuous across tiles (nk rounded up to even; the
 // pad K-tile stages zeros), so the next tile's first K-tiles are already in flight while the
 // finished tile's epilogue runs (between phases, beside the other wave-row's MFMAs).
-__device__ __forceinline__ bool pp_tile(const GemmP& p, int i, int& m0, int& n0, int& bz) {
-  const int vb = blockIdx.x + gridDim.x * i;
-  if (vb >= p.tiles_total) return false;
-  const int nwg = p.tiles_total;
-  const int q = nwg / 8, rr = nwg % 8, xcd = vb % 8;
-  const int tid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + vb / 8;
-  bz = tid / p.tiles_mn;
-  int mt, nt;
-  tile_coords(tid - bz * p.tiles_mn, p, mt, nt);
-  m0 = mt * 256;
-  n0 = nt * 256;
-  return true;
-}
 
+// PRIO (issue-priority scheme, A/B via flags bits 15-16): 0 = prio 1 around each MFMA phase;
+// 1 = static prio 1 for the trailing wave row (waves 4-7), no flips; 2 = no setprio;
+// 3 = static prio 1 for the leading row (waves 0-3)
+template <int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_REGION];
   const int lane = lane_id();
@@ -650,7 +234,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     sync();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -659,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
         for (int ni = 0; ni < 2; ++ni)
           acc[qm * 4 + mi][qn * 2 + ni] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[kk][ni], a[kk][mi], acc[qm * 4 + mi][qn * 2 + ni], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
     sync();
   };
 
@@ -673,6 +257,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
   sync();
   if (wm == 1) sync();                       // stagger the wave rows by one barrier
+  if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(1); }
+  if constexpr (PRIO == 3) { if (wm == 0) __builtin_amdgcn_s_setprio(1); }
 
   for (int g = 0; g < total; g += 2) {
     // K-tiles g, g+1 = (cur, kt), (cur, kt+1); g+2, g+3 = (nxt, k2), (nxt, k2+1)
@@ -709,6 +295,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // no LDS-DMA may outlive the block
   if (wm == 0) sync();                       // balance the stagger barrier
 }
+
 
 template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
 void launch(GemmP p, int batch, hipStream_t stream) {
@@ -884,7 +471,12 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
   p.tiles_total = p.tiles_mn * batch;
   int grid = p.tiles_total <= cus ? p.tiles_total : (cus & ~7);
   if (p.flags & 8192) grid = p.tiles_total;   // diagnostic: one tile per workgroup
-  hipLaunchKernelGGL(gemm_pp_kernel, dim3(grid), dim3(512), 0, stream, p);
+  switch ((p.flags >> 15) & 3) {
+    case 0: hipLaunchKernelGGL(gemm_pp_kernel<0>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 1: hipLaunchKernelGGL(gemm_pp_kernel<1>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL(gemm_pp_kernel<2>, dim3(grid), dim3(512), 0, stream, p); break;
+    default: hipLaunchKernelGGL(gemm_pp_kernel<3>, dim3(grid), dim3(512), 0, stream, p); break;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

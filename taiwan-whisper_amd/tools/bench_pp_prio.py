@@ -1,0 +1,62 @@
+"""A/B of the persistent ping-pong GEMM's issue-priority schemes (gemm_pp_kernel<PRIO>, flags bits 15-16)
+and its epilogue cost (p0s: no stores, p0e: no epilogue; diagnostic flags),
+interleaved in one process on random data, forward shapes of the distillation step."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch
+
+from tw import ops
+
+SHAPES = [("enc qkv", 96000, 3840, 1280, 0), ("enc out", 96000, 1280, 1280, 0), ("enc fc1", 96000, 5120, 1280, 1),
+          ("enc fc2", 96000, 1280, 5120, 0), ("xattn kv", 96000, 2560, 1280, 0), ("dec fc1", 28608, 5120, 1280, 1),
+          ("lm head", 28608, 51904, 1280, 0)]
+VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "p0,p0s,p0e").split(",")
+FLAG = {"p0": 0, "p1": 1 << 15, "p2": 2 << 15, "p3": 3 << 15, "p0e": 4096, "p0s": 1 << 21}
+
+
+def vflag(v):
+    return ops.GEMM_TILE256PP | FLAG[v]
+
+
+def main(rounds=5):
+    dev = "cuda"
+    for name, M, N, K, gelu in SHAPES:
+        A = torch.randn(M, K, device=dev).bfloat16()
+        W = torch.randn(N, K, device=dev).bfloat16()
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        bias = torch.randn(N, device=dev).bfloat16()
+        base = ops.GEMM_ROUND
+
+        def run(v):
+            if gelu:
+                ops.gemm(A, W, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bias, flags=base | ops.GEMM_GELU | vflag(v))
+            else:
+                ops.gemm(A, W, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bias, flags=base | vflag(v))
+        outs = {}
+        for v in VARIANTS:
+            run(v)
+            outs[v] = C.clone()
+        same = all(torch.equal(outs[v], outs[VARIANTS[0]]) for v in VARIANTS if len(v) < 3 or v == 'p0e')
+        times = {v: [] for v in VARIANTS}
+        for _ in range(rounds):
+            for v in VARIANTS:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    run(v)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / 3)
+        fl = 2.0 * M * N * K
+        line = f"{name:9s} M={M:6d} N={N:6d} K={K:5d} same={same} "
+        for v in VARIANTS:
+            t = sorted(times[v])[rounds // 2]
+            line += f" {v}: {fl / t / 1e9:7.1f}TF"
+        print(line, flush=True)
+        del A, W, C, outs
+
+
+if __name__ == "__main__":
+    main()

@@ -133,7 +133,8 @@ def test_gemm_forced_tiles_bit_identical(M, N, K):
             assert torch.equal(outs[name][kind], got), (name, kind)
 
 
-@pytest.mark.parametrize("M,N,K", [(8200, 2056, 320), (8200, 2056, 128), (4104, 4096, 1344), (520, 264, 64)])
+@pytest.mark.parametrize("M,N,K", [(8200, 2056, 320), (8200, 2056, 128), (4104, 4096, 1344), (520, 264, 64),
+                                   (2312, 1288, 5128)])
 def test_gemm_pp_persistent_ragged(M, N, K):
     """Persistent ping-pong kernel with more tiles than workgroups (the K-tile stream runs across
     tiles, the next tile's first K-tiles in flight during the epilogue; at K <= 128 every
