@@ -172,9 +172,10 @@ __device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_
 // pad K-tile stages zeros), so the next tile's first K-tiles are already in flight while the
 // finished tile's epilogue runs (between phases, beside the other wave-row's MFMAs).
 
-// PRIO (issue-priority scheme, A/B via flags bits 15-16): 0 = prio 1 around each MFMA phase;
-// 1 = static prio 1 for the trailing wave row (waves 4-7), no flips; 2 = no setprio;
-// 3 = static prio 1 for the leading row (waves 0-3)
+// PRIO (variant; flags bits 15-17 select it, see launch_pp): 0 = four 16-MFMA phases per K-tile,
+// prio 1 around each MFMA phase; 1 = the same with static prio 1 for the trailing wave row
+// (waves 4-7), no flips; 2 = diagnostic: every MFMA phase issued twice (wrong results; measures
+// the fixed per-phase cost); 4 = two 32-MFMA phases per K-tile (default: +4-8 % main loop)
 template <int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_REGION];
@@ -214,6 +215,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   };
 
   bf16x8 a[2][4], bb[2][2];
+  bf16x8 bq[2][2][2];                        // PRIO 4: both B-quarters of the K-tile
   auto rdA = [&](int b, int h) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -226,15 +228,43 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) bb[kk][ni] = frag_k(reg(b, 2 + qq), wn * 32 + ni * 16, kk, lane);
   };
+  auto rdB2 = [&](int b) {
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bq[qq][kk][ni] = frag_k(reg(b, 2 + qq), wn * 32 + ni * 16, kk, lane);
+  };
   auto sync = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
+  // PRIO 4: one phase = one A-half x both B-quarters (32 MFMAs)
+  auto mma2 = [&](int qm) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[qm * 4 + mi][qq * 2 + ni] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[qq][kk][ni], a[kk][mi], acc[qm * 4 + mi][qq * 2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     sync();
-    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 0 || PRIO == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int rep = 0; rep < (PRIO == 2 ? 2 : 1); ++rep)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -243,7 +273,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
         for (int ni = 0; ni < 2; ++ni)
           acc[qm * 4 + mi][qn * 2 + ni] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[kk][ni], a[kk][mi], acc[qm * 4 + mi][qn * 2 + ni], 0, 0, 0);
-    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 0 || PRIO == 2) __builtin_amdgcn_s_setprio(0);
     sync();
   };
 
@@ -253,12 +283,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   int kt = 0, ti = 0;
   stage(cm, cn, cb, ck, 0, 0, 0); stage(cm, cn, cb, ck, 0, 0, 1);
   stage(cm, cn, cb, ck, 0, 0, 2); stage(cm, cn, cb, ck, 0, 0, 3);
-  stage(cm, cn, cb, ck, 1, 1, 0); stage(cm, cn, cb, ck, 1, 1, 3); stage(cm, cn, cb, ck, 1, 1, 1);
+  if constexpr (PRIO == 4) {                 // K-tile 1 without its A-half 1 (staged in the first phase)
+    stage(cm, cn, cb, ck, 1, 1, 0); stage(cm, cn, cb, ck, 1, 1, 2); stage(cm, cn, cb, ck, 1, 1, 3);
+  } else {
+    stage(cm, cn, cb, ck, 1, 1, 0); stage(cm, cn, cb, ck, 1, 1, 3); stage(cm, cn, cb, ck, 1, 1, 1);
+  }
   asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
   sync();
   if (wm == 1) sync();                       // stagger the wave rows by one barrier
   if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(1); }
-  if constexpr (PRIO == 3) { if (wm == 0) __builtin_amdgcn_s_setprio(1); }
 
   for (int g = 0; g < total; g += 2) {
     // K-tiles g, g+1 = (cur, kt), (cur, kt+1); g+2, g+3 = (nxt, k2), (nxt, k2+1)
@@ -268,6 +301,29 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       tile_info(ti + 1, nm, nn, nb, nkl);
       k2 = 0;
     }
+    if constexpr (PRIO == 4) {
+      // Two phases per K-tile (A-half 0, then A-half 1, each against both B-quarters): the load
+      // segment before phase X reads A0, B0, B1 and stages A1 of the next K-tile; the one before
+      // phase Y reads A1 and stages A0, B0, B1 of the K-tile two ahead (their last readers, the
+      // other wave row's X-segment, finished one barrier earlier).  Waits, counted: at an X
+      // segment the A1 staged one segment-pair ago (6 DMA staged since), at a Y segment the
+      // A0/B0/B1 staged one pair ago (2 since) — each published by the barriers before its
+      // readers' segments.
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      rdA(0, 0); rdB2(0); stage(cm, cn, cb, ck, kt + 1, 1, 1);
+      mma2(0);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      rdA(0, 1);
+      stage(nm, nn, nb, nkl, k2, 0, 0); stage(nm, nn, nb, nkl, k2, 0, 2); stage(nm, nn, nb, nkl, k2, 0, 3);
+      mma2(1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      rdA(1, 0); rdB2(1); stage(nm, nn, nb, nkl, k2, 0, 1);
+      mma2(0);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      rdA(1, 1);
+      stage(nm, nn, nb, nkl, k2 + 1, 1, 0); stage(nm, nn, nb, nkl, k2 + 1, 1, 2); stage(nm, nn, nb, nkl, k2 + 1, 1, 3);
+      mma2(1);
+    } else {
     // even K-tile g from buffer 0
     rdB(0, 0); rdA(0, 0); stage(cm, cn, cb, ck, kt + 1, 1, 2);  mma(0, 0);
     rdB(0, 1);            stage(nm, nn, nb, nkl, k2, 0, 0);     mma(0, 1);
@@ -280,6 +336,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
     rdA(1, 1);            stage(nm, nn, nb, nkl, k2 + 1, 1, 3); mma(1, 1);
     rdB(1, 0);            stage(nm, nn, nb, nkl, k2 + 1, 1, 1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");            mma(1, 0);
+    }
     if (last) {                                                 // tile finished
       if (!(p.flags & 4096) || acc[0][0][0] != acc[0][0][0])    // 4096: diagnostic, skip epilogue
         epilogue<256, 256, 2, 4>(p, acc, cm, cn, wm, wn, lane, cb);
@@ -471,11 +528,17 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
   p.tiles_total = p.tiles_mn * batch;
   int grid = p.tiles_total <= cus ? p.tiles_total : (cus & ~7);
   if (p.flags & 8192) grid = p.tiles_total;   // diagnostic: one tile per workgroup
-  switch ((p.flags >> 15) & 3) {
-    case 0: hipLaunchKernelGGL(gemm_pp_kernel<0>, dim3(grid), dim3(512), 0, stream, p); break;
-    case 1: hipLaunchKernelGGL(gemm_pp_kernel<1>, dim3(grid), dim3(512), 0, stream, p); break;
+  // default: two 32-MFMA phases per K-tile (PRIO 4); flags bits 15-17 select the A/B variants
+  // (1: four 16-MFMA phases, per-phase priority = the previous default; 2..4 as documented above)
+  static const int env_variant = [] {
+    const char* e = getenv("TW_PP_VARIANT");   // A/B runs of whole steps only (bench.py)
+    return e ? atoi(e) : -1;
+  }();
+  switch (env_variant >= 0 ? env_variant : (p.flags >> 15) & 7) {
+    case 1: hipLaunchKernelGGL(gemm_pp_kernel<0>, dim3(grid), dim3(512), 0, stream, p); break;
     case 2: hipLaunchKernelGGL(gemm_pp_kernel<2>, dim3(grid), dim3(512), 0, stream, p); break;
-    default: hipLaunchKernelGGL(gemm_pp_kernel<3>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 3: hipLaunchKernelGGL(gemm_pp_kernel<1>, dim3(grid), dim3(512), 0, stream, p); break;
+    default: hipLaunchKernelGGL(gemm_pp_kernel<4>, dim3(grid), dim3(512), 0, stream, p); break;
   }
 }
 

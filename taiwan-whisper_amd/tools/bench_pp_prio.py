@@ -12,8 +12,9 @@ from tw import ops
 SHAPES = [("enc qkv", 96000, 3840, 1280, 0), ("enc out", 96000, 1280, 1280, 0), ("enc fc1", 96000, 5120, 1280, 1),
           ("enc fc2", 96000, 1280, 5120, 0), ("xattn kv", 96000, 2560, 1280, 0), ("dec fc1", 28608, 5120, 1280, 1),
           ("lm head", 28608, 51904, 1280, 0)]
-VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "p0,p0s,p0e").split(",")
-FLAG = {"p0": 0, "p1": 1 << 15, "p2": 2 << 15, "p3": 3 << 15, "p0e": 4096, "p0s": 1 << 21}
+VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "p4,p0,p4e").split(",")
+FLAG = {"p4": 0, "p4e": 4096, "p4s": 1 << 21, "p0": 1 << 15, "p0e": (1 << 15) | 4096,
+        "p2x": 2 << 15, "p2xe": (2 << 15) | 4096, "p1": 3 << 15}
 
 
 def vflag(v):
@@ -38,7 +39,7 @@ def main(rounds=5):
         for v in VARIANTS:
             run(v)
             outs[v] = C.clone()
-        same = all(torch.equal(outs[v], outs[VARIANTS[0]]) for v in VARIANTS if len(v) < 3 or v == 'p0e')
+        same = all(torch.equal(outs[v], outs[VARIANTS[0]]) for v in VARIANTS if v in ('p0', 'p1', 'p4'))
         times = {v: [] for v in VARIANTS}
         for _ in range(rounds):
             for v in VARIANTS:
@@ -53,7 +54,8 @@ def main(rounds=5):
         line = f"{name:9s} M={M:6d} N={N:6d} K={K:5d} same={same} "
         for v in VARIANTS:
             t = sorted(times[v])[rounds // 2]
-            line += f" {v}: {fl / t / 1e9:7.1f}TF"
+            mult = 2 if v.startswith("p2x") else 1       # doubled MFMA phases: twice the matrix work
+            line += f" {v}: {mult * fl / t / 1e9:7.1f}TF"
         print(line, flush=True)
         del A, W, C, outs
 
