@@ -198,22 +198,30 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   // the stream or the pad K-tile stages zeros, keeping the vmcnt counts uniform.
   // (plain scalars, no struct: a struct select here is promoted to LDS by the compiler, and any
   // LDS access it cannot disambiguate from the DMA costs a vmcnt(0) drain)
-  auto tile_info = [&](int i, int& m0, int& n0, int& bz, int& kl) {
+  // Tile state: the operand base pointers at k = 0, the rows / columns left and the K extent
+  // (0 past the stream: the stager then fills zeros); per K-tile the stager only adds kt * BK.
+  auto tile_info = [&](int i, const bf16*& pa, const bf16*& pb, int& rows, int& cols, int& kl) {
+    int m0 = 0, n0 = 0, bz = 0;
     const bool live = i < my_tiles && pp_tile(p, i, m0, n0, bz);
-    if (!live) { m0 = 0; n0 = 0; bz = 0; }
-    kl = live ? K : 0;                       // K extent seen by the stager (0: stage zeros)
+    pa = p.A + bz * p.sA + (int64_t)m0 * p.lda;
+    pb = p.B + bz * p.sB + (int64_t)n0 * p.ldb;
+    rows = p.M - m0;
+    cols = p.N - n0;
+    kl = live ? K : 0;
   };
   auto reg = [&](int b, int r) -> char* { return smem + (b * 4 + r) * PP_REGION; };
-  auto stage = [&](int m0, int n0, int bz, int kl, int kt, int buf, int r) {
+  auto stage = [&](const bf16* pa, const bf16* pb, int rows, int cols, int kl, int kt, int buf, int r) {
     const int k_left = kl - kt * BK;
     if (r < 2)
-      pp_stage<6, 128>(p.A + bz * p.sA + (int64_t)m0 * p.lda + kt * BK, p.lda, p.M - m0, k_left, r * 64,
-                       reg(buf, r), wave, lane);
+      pp_stage<6, 128>(pa + kt * BK, p.lda, rows, k_left, r * 64, reg(buf, r), wave, lane);
     else
-      pp_stage<5, 64>(p.B + bz * p.sB + (int64_t)n0 * p.ldb + kt * BK, p.ldb, p.N - n0, k_left, (r - 2) * 32,
-                      reg(buf, r), wave, lane);
+      pp_stage<5, 64>(pb + kt * BK, p.ldb, cols, k_left, (r - 2) * 32, reg(buf, r), wave, lane);
   };
 
+  // PRIO 6: diagnostic, no restaging in the main loop (timing of everything but the DMA)
+  auto stg = [&](const bf16* pa, const bf16* pb, int rows, int cols, int kl, int kt, int buf, int r) {
+    if constexpr (PRIO != 6) stage(pa, pb, rows, cols, kl, kt, buf, r);
+  };
   bf16x8 a[2][4], bb[2][2];
   bf16x8 bq[2][2][2];                        // PRIO 4: both B-quarters of the K-tile
   auto rdA = [&](int b, int h) {
@@ -278,15 +286,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   };
 
   // prologue: K-tile 0 whole into buffer 0, K-tile 1 without B-quarter 0 into buffer 1
-  int cm, cn, cb, ck;                        // current tile: m0, n0, batch, K extent
-  tile_info(0, cm, cn, cb, ck);
+  const bf16 *cpa, *cpb;                     // current tile (see tile_info)
+  int cr, cc, ck;
+  tile_info(0, cpa, cpb, cr, cc, ck);
   int kt = 0, ti = 0;
-  stage(cm, cn, cb, ck, 0, 0, 0); stage(cm, cn, cb, ck, 0, 0, 1);
-  stage(cm, cn, cb, ck, 0, 0, 2); stage(cm, cn, cb, ck, 0, 0, 3);
-  if constexpr (PRIO == 4) {                 // K-tile 1 without its A-half 1 (staged in the first phase)
-    stage(cm, cn, cb, ck, 1, 1, 0); stage(cm, cn, cb, ck, 1, 1, 2); stage(cm, cn, cb, ck, 1, 1, 3);
+  stage(cpa, cpb, cr, cc, ck, 0, 0, 0); stage(cpa, cpb, cr, cc, ck, 0, 0, 1);
+  stage(cpa, cpb, cr, cc, ck, 0, 0, 2); stage(cpa, cpb, cr, cc, ck, 0, 0, 3);
+  if constexpr (PRIO >= 4) {                 // K-tile 1 without its A-half 1 (staged in the first phase)
+    stage(cpa, cpb, cr, cc, ck, 1, 1, 0); stage(cpa, cpb, cr, cc, ck, 1, 1, 2); stage(cpa, cpb, cr, cc, ck, 1, 1, 3);
   } else {
-    stage(cm, cn, cb, ck, 1, 1, 0); stage(cm, cn, cb, ck, 1, 1, 3); stage(cm, cn, cb, ck, 1, 1, 1);
+    stage(cpa, cpb, cr, cc, ck, 1, 1, 0); stage(cpa, cpb, cr, cc, ck, 1, 1, 3); stage(cpa, cpb, cr, cc, ck, 1, 1, 1);
   }
   asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
   sync();
@@ -296,12 +305,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   for (int g = 0; g < total; g += 2) {
     // K-tiles g, g+1 = (cur, kt), (cur, kt+1); g+2, g+3 = (nxt, k2), (nxt, k2+1)
     const bool last = kt + 2 >= nke;
-    int nm = cm, nn = cn, nb = cb, nkl = ck, k2 = kt + 2;
+    const bf16 *npa = cpa, *npb = cpb;
+    int nr = cr, nc = cc, nkl = ck, k2 = kt + 2;
     if (last) {
-      tile_info(ti + 1, nm, nn, nb, nkl);
+      tile_info(ti + 1, npa, npb, nr, nc, nkl);
       k2 = 0;
     }
-    if constexpr (PRIO == 4) {
+    if constexpr (PRIO >= 4) {
       // Two phases per K-tile (A-half 0, then A-half 1, each against both B-quarters): the load
       // segment before phase X reads A0, B0, B1 and stages A1 of the next K-tile; the one before
       // phase Y reads A1 and stages A0, B0, B1 of the K-tile two ahead (their last readers, the
@@ -309,44 +319,48 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       // segment the A1 staged one segment-pair ago (6 DMA staged since), at a Y segment the
       // A0/B0/B1 staged one pair ago (2 since) — each published by the barriers before its
       // readers' segments.
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      rdA(0, 0); rdB2(0); stage(cm, cn, cb, ck, kt + 1, 1, 1);
+      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // PRIO 7: diagnostic, no waits
+      rdA(0, 0); rdB2(0); stg(cpa, cpb, cr, cc, ck, kt + 1, 1, 1);
       mma2(0);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      rdA(0, 1);
-      stage(nm, nn, nb, nkl, k2, 0, 0); stage(nm, nn, nb, nkl, k2, 0, 2); stage(nm, nn, nb, nkl, k2, 0, 3);
+      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if constexpr (PRIO == 4) rdA(0, 1);      // PRIO 5: diagnostic, A-half 1 not read (LDS-read cost)
+      stg(npa, npb, nr, nc, nkl, k2, 0, 0); stg(npa, npb, nr, nc, nkl, k2, 0, 2); stg(npa, npb, nr, nc, nkl, k2, 0, 3);
       mma2(1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      rdA(1, 0); rdB2(1); stage(nm, nn, nb, nkl, k2, 0, 1);
+      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // PRIO 7: diagnostic, no waits
+      rdA(1, 0); rdB2(1); stg(npa, npb, nr, nc, nkl, k2, 0, 1);
       mma2(0);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      rdA(1, 1);
-      stage(nm, nn, nb, nkl, k2 + 1, 1, 0); stage(nm, nn, nb, nkl, k2 + 1, 1, 2); stage(nm, nn, nb, nkl, k2 + 1, 1, 3);
+      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if constexpr (PRIO == 4) rdA(1, 1);
+      stg(npa, npb, nr, nc, nkl, k2 + 1, 1, 0); stg(npa, npb, nr, nc, nkl, k2 + 1, 1, 2); stg(npa, npb, nr, nc, nkl, k2 + 1, 1, 3);
       mma2(1);
     } else {
     // even K-tile g from buffer 0
-    rdB(0, 0); rdA(0, 0); stage(cm, cn, cb, ck, kt + 1, 1, 2);  mma(0, 0);
-    rdB(0, 1);            stage(nm, nn, nb, nkl, k2, 0, 0);     mma(0, 1);
-    rdA(0, 1);            stage(nm, nn, nb, nkl, k2, 0, 3);     mma(1, 1);
-    rdB(0, 0);            stage(nm, nn, nb, nkl, k2, 0, 1);
+    rdB(0, 0); rdA(0, 0); stage(cpa, cpb, cr, cc, ck, kt + 1, 1, 2);  mma(0, 0);
+    rdB(0, 1);            stage(npa, npb, nr, nc, nkl, k2, 0, 0);     mma(0, 1);
+    rdA(0, 1);            stage(npa, npb, nr, nc, nkl, k2, 0, 3);     mma(1, 1);
+    rdB(0, 0);            stage(npa, npb, nr, nc, nkl, k2, 0, 1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");            mma(1, 0);
     // odd K-tile g+1 from buffer 1
-    rdB(1, 0); rdA(1, 0); stage(nm, nn, nb, nkl, k2, 0, 2);     mma(0, 0);
-    rdB(1, 1);            stage(nm, nn, nb, nkl, k2 + 1, 1, 0); mma(0, 1);
-    rdA(1, 1);            stage(nm, nn, nb, nkl, k2 + 1, 1, 3); mma(1, 1);
-    rdB(1, 0);            stage(nm, nn, nb, nkl, k2 + 1, 1, 1);
+    rdB(1, 0); rdA(1, 0); stage(npa, npb, nr, nc, nkl, k2, 0, 2);     mma(0, 0);
+    rdB(1, 1);            stage(npa, npb, nr, nc, nkl, k2 + 1, 1, 0); mma(0, 1);
+    rdA(1, 1);            stage(npa, npb, nr, nc, nkl, k2 + 1, 1, 3); mma(1, 1);
+    rdB(1, 0);            stage(npa, npb, nr, nc, nkl, k2 + 1, 1, 1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");            mma(1, 0);
     }
     if (last) {                                                 // tile finished
       if (!(p.flags & 4096) || acc[0][0][0] != acc[0][0][0])    // 4096: diagnostic, skip epilogue
-        epilogue<256, 256, 2, 4>(p, acc, cm, cn, wm, wn, lane, cb);
+      {
+        int m0, n0, bz;
+        pp_tile(p, ti, m0, n0, bz);
+        epilogue<256, 256, 2, 4>(p, acc, m0, n0, wm, wn, lane, bz);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       ++ti;
     }
-    cm = nm; cn = nn; cb = nb; ck = nkl;
+    cpa = npa; cpb = npb; cr = nr; cc = nc; ck = nkl;
     kt = k2;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // no LDS-DMA may outlive the block
@@ -538,6 +552,9 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
     case 1: hipLaunchKernelGGL(gemm_pp_kernel<0>, dim3(grid), dim3(512), 0, stream, p); break;
     case 2: hipLaunchKernelGGL(gemm_pp_kernel<2>, dim3(grid), dim3(512), 0, stream, p); break;
     case 3: hipLaunchKernelGGL(gemm_pp_kernel<1>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 5: hipLaunchKernelGGL(gemm_pp_kernel<5>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 6: hipLaunchKernelGGL(gemm_pp_kernel<6>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 7: hipLaunchKernelGGL(gemm_pp_kernel<7>, dim3(grid), dim3(512), 0, stream, p); break;
     default: hipLaunchKernelGGL(gemm_pp_kernel<4>, dim3(grid), dim3(512), 0, stream, p); break;
   }
 }

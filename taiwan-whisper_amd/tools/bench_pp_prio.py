@@ -14,7 +14,7 @@ SHAPES = [("enc qkv", 96000, 3840, 1280, 0), ("enc out", 96000, 1280, 1280, 0), 
           ("lm head", 28608, 51904, 1280, 0)]
 VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "p4,p0,p4e").split(",")
 FLAG = {"p4": 0, "p4e": 4096, "p4s": 1 << 21, "p0": 1 << 15, "p0e": (1 << 15) | 4096,
-        "p2x": 2 << 15, "p2xe": (2 << 15) | 4096, "p1": 3 << 15}
+        "p2x": 2 << 15, "p2xe": (2 << 15) | 4096, "p1": 3 << 15, "p5e": (5 << 15) | 4096, "p6e": (6 << 15) | 4096, "p7e": (7 << 15) | 4096}
 
 
 def vflag(v):
