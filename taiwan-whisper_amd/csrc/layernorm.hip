@@ -194,18 +194,31 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x,
   }
 }
 
-// dw_out[c] += sum_b partial[b][0][c]; db_out[c] += sum_b partial[b][1][c]
-__global__ void ln_param_reduce_kernel(const float* __restrict__ partial, int nb, int D, float* __restrict__ dw_out,
-                                       float* __restrict__ db_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
+// dw_out[c] += sum_b partial[b][0][c]; db_out[c] += sum_b partial[b][1][c].  64 columns per
+// block; 16 thread rows each sum every 16th partial (coalesced 256-B rows, many loads in flight),
+// then a fixed-order combine in LDS (deterministic)
+__global__ __launch_bounds__(1024) void ln_param_reduce_kernel(const float* __restrict__ partial, int nb, int D,
+                                                               float* __restrict__ dw_out, float* __restrict__ db_out) {
+  __shared__ float sa[16][64], sb[16][64];
+  const int cl = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float a = 0.f, s = 0.f;
-  for (int b = 0; b < nb; ++b) {
-    a += partial[(int64_t)b * 2 * D + c];
-    s += partial[(int64_t)b * 2 * D + D + c];
+  if (c < D)
+    for (int b = j; b < nb; b += 16) {
+      a += partial[(int64_t)b * 2 * D + c];
+      s += partial[(int64_t)b * 2 * D + D + c];
+    }
+  sa[j][cl] = a;
+  sb[j][cl] = s;
+  __syncthreads();
+  if (j == 0 && c < D) {
+    for (int k = 1; k < 16; ++k) {
+      a += sa[k][cl];
+      s += sb[k][cl];
+    }
+    if (dw_out) dw_out[c] += a;
+    if (db_out) db_out[c] += s;
   }
-  if (dw_out) dw_out[c] += a;
-  if (db_out) db_out[c] += s;
 }
 
 }  // namespace
@@ -256,7 +269,7 @@ extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, cons
     hipLaunchKernelGGL((ln_bwd_kernel<1, 20>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy,
                        dy_dtype, dx, dx_accum, workspace, rows, D);
   TW_CHECK_LAUNCH();
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((D + 255) / 256), dim3(256), 0, stream, workspace, nblk, D, dw_out,
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((D + 63) / 64), dim3(1024), 0, stream, workspace, nblk, D, dw_out,
                      db_out);
   TW_CHECK_LAUNCH();
   return TW_OK;

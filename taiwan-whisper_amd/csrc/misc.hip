@@ -85,14 +85,23 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restr
   }
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ partial, int nchunk, int cols, float* __restrict__ out,
-                                    int accum, int round_bf16) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// out[c] = [out[c] +] round?(sum_k partial[k][c]): 64 columns per block, 16 thread rows each
+// summing every 16th chunk, fixed-order combine in LDS (deterministic)
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ partial, int nchunk, int cols,
+                                                            float* __restrict__ out, int accum, int round_bf16) {
+  __shared__ float st[16][64];
+  const int cl = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float t = 0.f;
-  for (int k = 0; k < nchunk; ++k) t += partial[(int64_t)k * cols + c];
-  if (round_bf16) t = rbf(t);
-  out[c] = accum ? out[c] + t : t;
+  if (c < cols)
+    for (int k = j; k < nchunk; k += 16) t += partial[(int64_t)k * cols + c];
+  st[j][cl] = t;
+  __syncthreads();
+  if (j == 0 && c < cols) {
+    for (int k = 1; k < 16; ++k) t += st[k][cl];
+    if (round_bf16) t = rbf(t);
+    out[c] = accum ? out[c] + t : t;
+  }
 }
 
 // sum of squares of a fp32 vector -> partial[blockIdx.x]
@@ -263,7 +272,7 @@ extern "C" int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int 
   if (workspace_floats < (int64_t)nchunk * cols) return TW_EINVAL;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + CS_COLS - 1) / CS_COLS, nchunk), dim3(256), 0, stream, x,
                      x_dtype, ldx, rows, cols, workspace);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, stream, workspace, nchunk, cols, out,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64), dim3(1024), 0, stream, workspace, nchunk, cols, out,
                      accum, round_bf16);
   TW_CHECK_LAUNCH();
   return TW_OK;
