@@ -665,7 +665,12 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
     const char* e = getenv("TW_GEMM_GROUP_M");   // A/B sweeps only (tools/bench_gemm.py)
     return e ? atoi(e) : 0;
   }();
-  p.group_m = env_group > 0 ? env_group : 1;
+  // tile order: runs of 8 m-tiles walked n-tile by n-tile for the tall, short-K forward GEMMs (the
+  // encoder's M = B x 1500 projections: +3-5 % from L2 reuse of the weight panels,
+  // tools/bench_pp_prio.py with TW_GEMM_GROUP_M); plain row-major elsewhere (K = 5120 and the
+  // decoder's M = B x 447 shapes lose with grouping)
+  const bool grouped = !a_trans && !b_trans && batch == 1 && M >= 65536 && K <= 2048;
+  p.group_m = env_group > 0 ? env_group : (grouped ? 8 : 1);
   p.epi = pick_epilogue(p, batch);
   // 256x256 tiles (8 waves) when the problem has enough tiles to fill the chip, else 128x128
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
