@@ -85,6 +85,89 @@ def test_gemm_epilogues():
     assert (C4.float().cpu() - x.grad).abs().max() <= 2 ** -7 * x.grad.abs().max() + 1e-6
 
 
+def _gelu_exact_bf16_bits():
+    """bf16 bits of GELU for every bf16 bit pattern: PyTorch's erf-form formula in fp32 (reference),
+    x * 0.5 * (1 + erf(x * M_SQRT1_2)) (the reference's autocast F.gelu), with a correctly rounded
+    fp32 erf (math.erf in double, rounded once), then bf16 round-to-nearest-even;
+    +inf -> +inf, -inf -> -0, NaN -> NaN (the kernels' stated edge behaviour)."""
+    bits = np.arange(1 << 16, dtype=np.uint32)
+    with np.errstate(invalid="ignore"):
+        x = (bits << 16).view(np.float32).copy()
+        xa = x * np.float32(0.70710678118654752440)
+    fin = np.isfinite(x)
+    e = np.zeros_like(x)
+    e[fin] = np.array([math.erf(v) for v in xa[fin].astype(np.float64).tolist()]).astype(np.float32)
+    with np.errstate(invalid="ignore"):
+        g = (x * np.float32(0.5)) * (np.float32(1.0) + e)
+    out = torch.from_numpy(g).bfloat16().view(torch.int16).numpy().view(np.uint16).copy()
+    out[np.isposinf(x)] = 0x7f80
+    out[np.isneginf(x)] = 0x8000
+    out[np.isnan(x)] = 0x7fc0
+    return bits.astype(np.uint16), out
+
+
+def test_gemm_gelu_exhaustive():
+    """The GELU epilogue on all 65536 bf16 inputs through every GEMM path that applies it: the
+    persistent ping-pong, 128², 256² and 256x128 tiles (packed fast epilogue; a ragged column tail
+    -> generic epilogue) and the skinny decode kernel (per-element epilogue).  Inputs enter as the
+    bias of a zero product, so the pre-activation is exactly the bf16 pattern (checked through the
+    aux output).  Every path returns the same bits (one operation sequence, common.h gelu_erf /
+    gelu_erf2), within 1 bf16 ulp of PyTorch's fp32 formula or 5e-7 absolute (the negative tail
+    x < -4.5, |GELU| < 2e-5: the A&S erf's 1.5e-7 absolute error and PyTorch's 1 + erf cancellation
+    both exceed an ulp there)."""
+    from tw import ops
+    xb, want = _gelu_exact_bf16_bits()
+    n_all = xb.size
+    bias = torch.from_numpy(xb.view(np.int16).copy()).view(torch.bfloat16).to(DEV)
+    with np.errstate(invalid="ignore"):
+        xf = (xb.astype(np.uint32) << 16).view(np.float32)
+    finite = torch.from_numpy(np.isfinite(xf))
+    plain = finite & (torch.arange(n_all) != 0x8000)      # 0 + bias: -0 enters as +0
+    wv = torch.from_numpy(want.view(np.int16).copy()).view(torch.bfloat16).float()
+    outs = {}
+
+    def check(C, cols, what):
+        got = C.float().cpu()
+        assert torch.equal(C[0].view(torch.int16).cpu(), C[-1].view(torch.int16).cpu()), what
+        g, w, f = got[0], wv[cols], finite[cols]
+        tol = torch.maximum(w.abs() * 2 ** -7, torch.full_like(w, 5e-7))
+        bad = (f & ((g - w).abs() > tol)).nonzero().flatten()
+        assert bad.numel() == 0, (what, [(float(xf[cols][i]), float(g[i]), float(w[i])) for i in bad[:8].tolist()])
+        outs[what] = C[0].view(torch.int16).cpu()
+
+    K = 64
+    for name, f, M in (("pp", ops.GEMM_TILE256PP, 256), ("t128", ops.GEMM_TILE128, 128),
+                       ("t256", ops.GEMM_TILE256, 256), ("s3", ops.GEMM_TILE256x128, 256)):
+        for N in (n_all, n_all - 40):                   # full tiles; a ragged column tail
+            A = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+            W = torch.zeros(N, K, dtype=torch.bfloat16, device=DEV)
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            ops.gemm(A, W, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bias[:N], aux=aux, ldaux=N,
+                     flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT | f)
+            torch.cuda.synchronize()
+            pre = aux[0].view(torch.int16).cpu()
+            assert torch.equal(pre[plain[:N]], bias[:N].view(torch.int16).cpu()[plain[:N]])
+            check(C, slice(0, N), f"{name}/{N}")
+    # skinny decode kernel (M <= 128, N <= 4096 per call)
+    M, parts = 5, []
+    for c0 in range(0, n_all, 4096):
+        N = 4096
+        A = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+        W = torch.zeros(N, K, dtype=torch.bfloat16, device=DEV)
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(A, W, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bias[c0:c0 + N], flags=ops.GEMM_ROUND | ops.GEMM_GELU)
+        torch.cuda.synchronize()
+        check(C, slice(c0, c0 + N), f"skinny/{c0}")
+        parts.append(outs.pop(f"skinny/{c0}"))
+    outs["skinny"] = torch.cat(parts)
+    ref = outs["pp/%d" % n_all]
+    fin = finite.clone()
+    for k, v in outs.items():                                # one operation sequence on every path
+        n = v.numel()
+        assert torch.equal(v[fin[:n]], ref[:n][fin[:n]]), k
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 264, 200), (520, 600, 1344), (1000, 784, 1280), (256, 256, 64)])
 def test_gemm_forced_tiles_bit_identical(M, N, K):
     """Every tile variant (128², 256², 256x128 3-stage ring, 256² ping-pong) accumulates each output
