@@ -267,23 +267,27 @@ class WhisperTokenizerAdapter:
 
 
 # ----------------------------------------------------------------------------------- sharding
-def shard_micro_batches(n_items: int, batch_size: int, rank: int, world: int, order: Optional[Sequence[int]] = None):
+def shard_micro_batches(n_items: int, batch_size: int, rank: int, world: int, order: Optional[Sequence[int]] = None,
+                        with_real: bool = False):
     """Item indices of the micro-batches rank `rank` consumes: global micro-batch j holds stream
     positions [j*B, (j+1)*B); rank r takes j = k*world + r.  The last group of `world` micro-batches
     is completed from the start of the stream (accelerate even_batches), so all ranks get the same
-    number of full micro-batches."""
+    number of full micro-batches.  with_real=True also returns, per micro-batch, how many of its
+    leading items are real (stream position < n_items) -- the rows accelerate's gather_for_metrics
+    keeps on the last batch (it truncates the rank-major gathered rows to the dataset remainder)."""
     order = list(range(n_items)) if order is None else list(order)
     if not order:
-        return []
+        return ([], []) if with_real else []
     group = batch_size * world
     n_groups = -(-len(order) // group)
     need = n_groups * group
     stream = [order[i % len(order)] for i in range(need)]
-    out = []
+    out, real = [], []
     for k in range(n_groups):
         j = k * world + rank
         out.append(stream[j * batch_size:(j + 1) * batch_size])
-    return out
+        real.append(max(0, min(batch_size, len(order) - j * batch_size)))
+    return (out, real) if with_real else out
 
 
 # -------------------------------------------------------------------------------- preparation
@@ -324,7 +328,8 @@ class DataFeed:
         order = list(range(len(dataset)))
         if shuffle:
             np.random.Generator(np.random.PCG64(seed + epoch)).shuffle(order)
-        self.batches = shard_micro_batches(len(order), batch_size, rank, world, order)[skip_batches:]
+        batches, real = shard_micro_batches(len(order), batch_size, rank, world, order, with_real=True)
+        self.batches, self.n_real = batches[skip_batches:], real[skip_batches:]
         self.rng = np.random.Generator(np.random.PCG64([seed, epoch, rank]))
         self.prep_kw = prep_kw
         self.fe = WhisperFeatureExtractor(device=self.device)
@@ -342,7 +347,7 @@ class DataFeed:
 
     def _submit(self):
         while len(self._futs) < self.depth and self._next < len(self.batches):
-            self._futs.append(self.pool.submit(self._host, self.batches[self._next]))
+            self._futs.append((self.pool.submit(self._host, self.batches[self._next]), self.n_real[self._next]))
             self._next += 1
 
     def __iter__(self):
@@ -353,7 +358,8 @@ class DataFeed:
         if not self._futs:
             self.pool.shutdown(wait=False)
             raise StopIteration
-        feats = self._futs.pop(0).result()
+        fut, n_real = self._futs.pop(0)
+        feats = fut.result()
         self._submit()
         # label sampling stays on this thread: one rng, stream order (deterministic per rank)
         wavs, dec, lab = prepare_train_batch(feats, self.tok, self.rng, **self.prep_kw)
@@ -366,4 +372,4 @@ class DataFeed:
         mel, conv = self.fe.extract(wav, want_conv_input=True)
         return {"conv_input": conv, "input_features": mel,
                 "decoder_input_ids": dec.to(self.device, non_blocking=True),
-                "labels": lab.to(self.device, non_blocking=True)}
+                "labels": lab.to(self.device, non_blocking=True), "n_real": n_real}

@@ -35,6 +35,42 @@ def linear_schedule(step: int, warmup: int, total: int) -> float:
     return max(0.0, (total - step) / max(1, total - warmup))
 
 
+def set_trainable_like_reference(student: WhisperForConditionalGeneration, freeze_encoder: bool,
+                                 freeze_decoder: bool, freeze_embed_positions: bool):
+    """The trainable set of run_distillation.py:1043-1066 (HF keeps encoder.embed_positions frozen;
+    with freeze_decoder the tied proj_out = embed_tokens stays trainable)."""
+    student.set_trainable("", True)
+    student.set_trainable("model.encoder.embed_positions", False)
+    if freeze_encoder:
+        student.set_trainable("model.encoder", False)
+    if freeze_decoder:
+        student.set_trainable("model.decoder", False)
+        student.set_trainable("model.decoder.embed_tokens", True)
+    if freeze_embed_positions:
+        student.set_trainable("model.decoder.embed_positions", False)
+    return student
+
+
+def weight_decay_runs(s: WhisperForConditionalGeneration, wd: float, freeze_encoder: bool, freeze_decoder: bool):
+    """Maximal [lo, hi) ranges of the packed trainable prefix sharing one weight decay.  The decay set is
+    the reference's group 0 (run_distillation.py:1424-1449: get_parameter_names(student, [LayerNorm],
+    forbidden_module=[frozen encoder / decoder]) minus "bias" names) -- the same rule
+    tw/checkpoint.optimizer_groups writes into optimizer.bin, so with freeze_decoder the trainable
+    embed_tokens (under the frozen decoder module) is NOT decayed."""
+    from .checkpoint import optimizer_groups
+    decay = set(optimizer_groups(s.config, freeze_encoder, freeze_decoder)[0])
+    runs = []
+    for n in s.train_names:
+        w = wd if n in decay else 0.0          # the pseudo k_proj.zero_bias segments are never decayed
+        lo = s.store.offset[n]
+        hi = (lo + s.store.numel(n) + 63) // 64 * 64
+        if runs and runs[-1][2] == w and runs[-1][1] == lo:
+            runs[-1][1] = hi
+        else:
+            runs.append([lo, hi, w])
+    return [tuple(r) for r in runs]
+
+
 class DistillationTrainer:
     def __init__(self, student: WhisperForConditionalGeneration, teacher: WhisperForConditionalGeneration, *,
                  temperature: float = 2.0, kl_weight: float = 1.0, learning_rate: float = 1e-4,
@@ -52,16 +88,7 @@ class DistillationTrainer:
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.bucket = dp_bucket_mb * (1 << 20) // 4
-        # trainable set (run_distillation.py:1043-1066; HF keeps encoder.embed_positions frozen)
-        student.set_trainable("", True)
-        student.set_trainable("model.encoder.embed_positions", False)
-        if freeze_encoder:
-            student.set_trainable("model.encoder", False)
-        if freeze_decoder:
-            student.set_trainable("model.decoder", False)
-            student.set_trainable("model.decoder.embed_tokens", True)   # proj_out stays trainable
-        if freeze_embed_positions:
-            student.set_trainable("model.decoder.embed_positions", False)
+        set_trainable_like_reference(student, freeze_encoder, freeze_decoder, freeze_embed_positions)
         self.train_encoder = not freeze_encoder
         self.freeze_encoder, self.freeze_decoder = freeze_encoder, freeze_decoder
         self.share = freeze_encoder and student.config.d_model == teacher.config.d_model
@@ -81,20 +108,7 @@ class DistillationTrainer:
         self.runs = self._wd_runs()
 
     def _wd_runs(self):
-        """maximal [lo, hi) ranges of the trainable prefix sharing one weight decay
-        (decay group = non-LayerNorm, non-bias names, run_distillation.py:1434-1449)."""
-        s = self.s
-        runs = []
-        for n in s.train_names:
-            wd = 0.0 if ("layer_norm" in n or "bias" in n) else self.wd
-            lo = s.store.offset[n]
-            hi = lo + s.store.numel(n)
-            hi = (hi + 63) // 64 * 64
-            if runs and runs[-1][2] == wd and runs[-1][1] == lo:
-                runs[-1][1] = hi
-            else:
-                runs.append([lo, hi, wd])
-        return [tuple(r) for r in runs]
+        return weight_decay_runs(self.s, self.wd, self.freeze_encoder, self.freeze_decoder)
 
     def num_trainable_parameters(self):
         return self.s.num_parameters(only_trainable=True)
@@ -123,9 +137,13 @@ class DistillationTrainer:
             ht = t.decode(ids, enc_t, Tk)
         return t.lm_head(ht)
 
-    def train_step(self, batch, temperature: Optional[float] = None):
+    def train_step(self, batch, temperature: Optional[float] = None, end_of_dataloader: bool = False):
         """One micro-step: student fwd + teacher fwd + fused KL/CE + backward (+ DP exchange,
-        clip and AdamW on the sync micro-step).  Returns device scalars."""
+        clip and AdamW on the sync micro-step).  Returns device scalars.
+
+        Sync micro-step = every `accum`-th one, or the last batch of the dataloader (accelerate's
+        GradientState syncs at end_of_dataloader and restarts its count, ACC accelerator.py _do_sync):
+        the partial accumulation -- k < accum gradients, each already scaled by 1/accum -- is applied."""
         T = self.temperature if temperature is None else temperature
         s = self.s
         conv_in = self._conv_input(batch)
@@ -137,7 +155,8 @@ class DistillationTrainer:
         # DP: on the micro-step that syncs, each layer's gradient slice is all-reduced as soon as
         # the backward has finished it (RCCL on its own stream, beside the remaining backward)
         self._pending, self._reduced = [], []
-        self.bw.on_ready = self._grad_ready if (self.world > 1 and self.micro + 1 == self.accum) else None
+        sync = self.micro + 1 == self.accum or end_of_dataloader
+        self.bw.on_ready = self._grad_ready if (self.world > 1 and sync) else None
         enc_tape = [] if self.train_encoder else None
         enc16 = s.encode(conv_in, tape=enc_tape)
         Tk = enc16.shape[0] // B
@@ -159,7 +178,7 @@ class DistillationTrainer:
         if self.train_encoder:
             self.bw.encoder(enc_tape, d_enc)
         self.micro += 1
-        if self.micro == self.accum:
+        if sync:
             self.optimizer_step()
             self.micro = 0
         return {"loss": out3[0], "ce_loss": out3[1], "kl_loss": out3[2]}

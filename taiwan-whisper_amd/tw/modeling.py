@@ -41,6 +41,11 @@ def padded_vocab(V: int) -> int:
     return (V + 63) // 64 * 64
 
 
+
+def fp32_compute_supported() -> bool:
+    """True once the fp32-arithmetic path (mixed_precision="no") is built into libtw_hip.so."""
+    return False
+
 # ---------------------------------------------------------------------------------------------
 # parameter layout
 def _attn_segs(p, d, fused_kv_only=False):

@@ -135,37 +135,80 @@ def _mean_over_ranks(metrics: dict, world: int) -> dict:
     return {k: float(x) for k, x in zip(keys, v.tolist())}
 
 
+def gather_eval_rows(rows, world: int):
+    """[(batch index, preds, labels)] of every rank -> flat preds / labels in gather_for_metrics order
+    (batch-major, then rank)."""
+    gathered = [rows]
+    if world > 1:
+        gathered = [None] * world
+        torch.distributed.all_gather_object(gathered, rows)
+    merged = sorted(((bi, r, p, l) for r, rk in enumerate(gathered) for bi, p, l in rk), key=lambda x: (x[0], x[1]))
+    preds = [x for _, _, p, _ in merged for x in p]
+    labels = [x for _, _, _, l in merged for x in l]
+    return preds, labels
+
+
 def evaluate(trainer, feed, tokenizer, gen_kwargs: dict, predict_with_generate: bool, world: int,
              return_timestamps: bool = False):
-    """The eval block of the loop (:1709-1800): mean of eval_step metrics over batches (and ranks),
-    greedy generation of every batch, MER (x100) on decoded strings gathered from all ranks."""
+    """The eval block of the loop (:1709-1800): mean of the eval_step metrics over every (batch, rank)
+    scalar (torch.mean of the gathered per-rank scalars), greedy generation of every batch, MER (x100)
+    on the decoded strings of all ranks.  Predictions / labels follow gather_for_metrics: gathered
+    batch by batch in rank order, the wrap-around duplicates of the last (even_batches) group dropped
+    (batch["n_real"] from DataFeed), so each eval item is scored exactly once."""
     from .evaluation import compute_metrics
     sums, n = None, 0
-    preds, labels = [], []
-    for batch in feed:
+    rows = []                      # (batch index, preds, labels) of this rank, duplicates dropped
+    for bi, batch in enumerate(feed):
         m = trainer.eval_step(batch)
         v = torch.stack([m["loss"], m["ce_loss"], m["kl_loss"]]).float()
         sums = v if sums is None else sums + v
         n += 1
         if predict_with_generate:
+            keep = int(batch.get("n_real", batch["labels"].shape[0]))
             ids = trainer.s.generate(batch["input_features"], **gen_kwargs)
-            preds.extend(r.tolist() for r in ids.cpu())
-            labels.extend(r.tolist() for r in batch["labels"].cpu())
+            rows.append((bi, [r.tolist() for r in ids[:keep].cpu()], [r.tolist() for r in batch["labels"][:keep].cpu()]))
     if world > 1:
         torch.distributed.all_reduce(sums)
         cnt = torch.tensor([float(n)], device=sums.device)
         torch.distributed.all_reduce(cnt)
         n = int(cnt.item())
-        if predict_with_generate:
-            gathered = [None] * world
-            torch.distributed.all_gather_object(gathered, (preds, labels))
-            preds = [p for g in gathered for p in g[0]]
-            labels = [l for g in gathered for l in g[1]]
+    preds, labels = gather_eval_rows(rows, world) if predict_with_generate else ([], [])
     out = {k: float(x) / max(n, 1) for k, x in zip(("loss", "ce_loss", "kl_loss"), sums.tolist())} if sums is not None else {}
     if predict_with_generate and preds:
         wer, *_ = compute_metrics(preds, labels, tokenizer, return_timestamps=return_timestamps)
         out.update(wer)
     return out
+
+
+def teacher_dtype(dtype: str):
+    """--dtype -> teacher weight dtype (run_distillation.py:815-823).  bfloat16 = bf16 autocast
+    (mixed_precision="bf16"); float32 = mixed_precision="no" (fp32 arithmetic end to end, the
+    reference's default).  float16 (fp16 autocast + grad scaler) is not implemented and raises
+    rather than silently running another precision."""
+    if dtype == "bfloat16":
+        return torch.bfloat16
+    if dtype == "float32":
+        from .modeling import fp32_compute_supported
+        if not fp32_compute_supported():
+            raise NotImplementedError("--dtype float32 (mixed_precision='no') needs the fp32 arithmetic path")
+        return torch.float32
+    raise NotImplementedError(f"--dtype {dtype}: only bfloat16 and float32 are implemented (fp16 autocast "
+                              "with a dynamic loss scaler is not)")
+
+
+def load_models(args, device, tokenizer=None):
+    """Teacher (in --dtype) and fp32-master student, as run_distillation.py:1009-1031 loads them; with
+    --mix_lang_emb only the TEACHER is mixed (:1019-1020) — the student's <|zh|> row was mixed once at
+    creation (create_student_model.py:124-125)."""
+    from .modeling import WhisperForConditionalGeneration
+    from .student import mix_language_embeddings
+    teacher = WhisperForConditionalGeneration.from_pretrained(args.teacher_model_name_or_path,
+                                                              torch_dtype=teacher_dtype(args.dtype), device=device)
+    student = WhisperForConditionalGeneration.from_pretrained(args.model_name_or_path, device=device)
+    if args.mix_lang_emb:
+        mix_language_embeddings(teacher, tokenizer if hasattr(tokenizer, "convert_tokens_to_ids") else None,
+                                languages=["zh", "en"])
+    return teacher, student
 
 
 def main(argv=None):
@@ -181,14 +224,8 @@ def main(argv=None):
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(args.seed)
     os.makedirs(args.output_dir, exist_ok=True)
-    tdtype = {"bfloat16": torch.bfloat16, "float16": torch.bfloat16, "float32": torch.float32}[args.dtype]
-    teacher = WhisperForConditionalGeneration.from_pretrained(args.teacher_model_name_or_path, torch_dtype=tdtype,
-                                                              device=dev)
-    student = WhisperForConditionalGeneration.from_pretrained(args.model_name_or_path, device=dev)
     tokenizer = load_tokenizer(args)
-    if args.mix_lang_emb:
-        mix_language_embeddings(student, tokenizer if hasattr(tokenizer, "convert_tokens_to_ids") else None)
-        mix_language_embeddings(teacher, tokenizer if hasattr(tokenizer, "convert_tokens_to_ids") else None)
+    teacher, student = load_models(args, dev, tokenizer)
     trainer = DistillationTrainer(
         student, teacher, temperature=args.temperature, kl_weight=args.kl_weight, learning_rate=args.learning_rate,
         adam_beta1=args.adam_beta1, adam_beta2=args.adam_beta2, adam_epsilon=args.adam_epsilon,
@@ -229,8 +266,9 @@ def main(argv=None):
         feed = DataFeed(train_ds, tokenizer, args.per_device_train_batch_size, rank=rank, world=world, device=dev,
                         seed=args.seed, epoch=epoch, skip_batches=skip, workers=args.dataloader_num_workers, **prep)
         skip = 0
-        for batch in feed:
-            m = trainer.train_step(batch, temperature=args.temperature)
+        n_batches = len(feed)
+        for bi, batch in enumerate(feed):
+            m = trainer.train_step(batch, temperature=args.temperature, end_of_dataloader=bi + 1 == n_batches)
             if trainer.micro != 0:
                 continue                                     # accumulating
             cur_step += 1

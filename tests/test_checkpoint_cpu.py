@@ -86,3 +86,38 @@ def test_resume_skip_batches():
     assert resume_skip_batches(250, 2, 100, accum=4, streaming=False, max_steps=-1) == 200
     assert resume_skip_batches(250, 2, 100, accum=1, streaming=True, max_steps=-1) is None
     assert resume_skip_batches(250, 2, 100, accum=1, streaming=False, max_steps=1000) is None
+
+
+@pytest.mark.parametrize("freeze_encoder,freeze_decoder", [(True, False), (False, False), (True, True)])
+def test_weight_decay_runs_follow_reference_groups(freeze_encoder, freeze_decoder):
+    """The AdamW launches' per-range weight decay (tw.distill.weight_decay_runs over the packed flat
+    store) equals the group each parameter sits in inside the reference's torch AdamW
+    (run_distillation.py:1424-1456, rebuilt here from an HF module tree), so the update and the
+    optimizer.bin groups agree -- incl. freeze_decoder, where the trainable embed_tokens lives under a
+    forbidden module and gets weight_decay 0."""
+    from tw.config import WhisperConfig
+    from tw.distill import set_trainable_like_reference, weight_decay_runs
+    from tw.modeling import WhisperForConditionalGeneration
+    cfg = CONFIGS["micro"]
+    m = _hf(cfg)
+    forbidden = [x for x, f in ((m.model.encoder, freeze_encoder), (m.model.decoder, freeze_decoder)) if f]
+    decay = set(n for n in _reference_parameter_names(m, [torch.nn.LayerNorm], forbidden_module=forbidden)
+                if "bias" not in n)
+    s = WhisperForConditionalGeneration(WhisperConfig(**cfg), device="cpu")
+    set_trainable_like_reference(s, freeze_encoder, freeze_decoder, True)
+    s.pack_for_training()
+    runs = weight_decay_runs(s, 0.01, freeze_encoder, freeze_decoder)
+    assert all(runs[i][1] <= runs[i + 1][0] for i in range(len(runs) - 1))
+    assert runs[0][0] == 0 and runs[-1][1] <= s.train_prefix
+    checked = 0
+    for n in s.train_names:
+        if n.endswith(".zero_bias"):
+            continue
+        o = s.store.offset[n]
+        wd = [w for lo, hi, w in runs if lo <= o < hi]
+        assert len(wd) == 1, n
+        assert wd[0] == (0.01 if n in decay else 0.0), (n, wd[0])
+        checked += 1
+    assert checked == len(s.trainable)
+    if freeze_decoder:
+        assert "model.decoder.embed_tokens.weight" in s.trainable and "model.decoder.embed_tokens.weight" not in decay

@@ -89,6 +89,15 @@ def test_shard_micro_batches():
     seen = sorted(i for s in shards for mb in s for i in mb)
     assert set(seen) == set(range(13))
     assert D.shard_micro_batches(0, 4, 0, 2) == []
+    # real-item counts: stream positions < 13 are real, the wrapped tail is duplicates
+    for r in range(N):
+        mbs, real = D.shard_micro_batches(13, B, r, N, with_real=True)
+        assert mbs == shards[r]
+        for k, n in enumerate(real):
+            j = k * N + r
+            assert n == sum(1 for pos in range(j * B, (j + 1) * B) if pos < 13)
+    total_real = sum(n for r in range(N) for n in D.shard_micro_batches(13, B, r, N, with_real=True)[1])
+    assert total_real == 13
 
 
 def test_prepare_train_batch_matches_oracle():

@@ -126,3 +126,30 @@ def test_dp_mean_equals_accumulation_on_oracle():
         acc = g if acc is None else acc + g
     for r in range(world):
         assert torch.allclose(out[r], acc, rtol=1e-5, atol=1e-7)
+
+
+def _worker_eval_gather(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "taiwan-whisper_amd"))
+    from tw.dataset import shard_micro_batches
+    from tw.run_distillation import gather_eval_rows
+    _init(rank, world, port)
+    n_items, B = 11, 2
+    mbs, real = shard_micro_batches(n_items, B, rank, world, with_real=True)
+    # a "prediction" row per item that names the item, so duplicates would be visible
+    rows = [(bi, [[i, 7] for i in mb[:k]], [[i] for i in mb[:k]]) for bi, (mb, k) in enumerate(zip(mbs, real))]
+    out[rank] = gather_eval_rows(rows, world)
+    dist.destroy_process_group()
+
+
+def test_eval_gather_drops_even_batches_duplicates():
+    """Eval predictions are gathered like accelerate's gather_for_metrics: every item once, in
+    batch-major / rank order (11 items, B = 2, world 3: the last group wraps 1 item around)."""
+    world = 3
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_worker_eval_gather, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        preds, labels = out[r]
+        assert [p[0] for p in preds] == list(range(11))
+        assert labels == [[i] for i in range(11)]

@@ -258,6 +258,39 @@ def test_gemm_pp_persistent_ragged(M, N, K):
     assert bool((big[:, N:] == 7.0).all())
 
 
+def test_gemm_pp_grouped_tile_order():
+    """The production tile order of the encoder projections (M >= 65536, K <= 2048: runs of 8 m-tiles
+    walked n-tile by n-tile) with a ragged last m-group (ceil(66000 / 256) = 258 m-tiles, 258 % 8 = 2)
+    and ragged M: bit-identical to the 128x128 kernel (same K order) for the plain, GELU and in-place
+    residual epilogues, and sampled rows within one bf16 ulp of fp64."""
+    from tw import ops
+    M, N, K = 66000, 1280, 1280
+    g = torch.Generator().manual_seed(5)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    res0 = bf(torch.randn(M, N, generator=g)).to(DEV)
+    outs = {}
+    for name, f in (("t128", ops.GEMM_TILE128), ("pp", 0)):
+        o = {}
+        for kind, extra in (("bf16", 0), ("gelu", ops.GEMM_GELU)):
+            C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+            ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, flags=ops.GEMM_ROUND | extra | f)
+            o[kind] = C
+        rb = res0.clone()
+        ops.gemm(Ad, Wd, rb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rb, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_bf16"] = rb
+        outs[name] = o
+    torch.cuda.synchronize()
+    for kind in ("bf16", "gelu", "res_bf16"):
+        assert not torch.isnan(outs["pp"][kind]).any(), kind
+        assert torch.equal(outs["pp"][kind], outs["t128"][kind]), kind
+    rows = torch.tensor([0, 255, 256 * 8 - 1, 256 * 8, 256 * 256 + 3, M - 1])
+    ref = bf((bf(A[rows]).double() @ bf(W).double().T + bf(bias).double()).float()).float()
+    got = outs["pp"]["bf16"][rows.to(DEV)].float().cpu()
+    assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
+
+
 @pytest.mark.parametrize("N,K,M", [(1280, 1280, 28608), (2560, 1280, 8192), (264, 136, 4096), (1280, 1280, 1000)])
 def test_gemm_splitk_weight_grad(N, K, M):
     """dW[N][K] += round(dY^T X) with dY [M][N], X [M][K] (both MN-major operands, fp32 accumulate): the

@@ -115,3 +115,34 @@ def test_entry_point_train_eval_resume(tmp_path):
     from oracle.weights import CONFIGS
     with open(os.path.join(out, "config.json")) as f:
         assert json.load(f)["d_model"] == CONFIGS["micro"]["d_model"]
+
+
+def test_partial_accumulation_steps_at_end_of_dataloader():
+    """accelerate syncs at end_of_dataloader: with accum 2 and 3 micro-batches in an epoch the third
+    micro-batch's (1/accum-scaled) gradient is applied by a second update instead of leaking into the
+    next epoch's accumulation."""
+    from oracle import labels as L
+    from oracle.weights import CONFIGS, make_weights
+    from tw.config import WhisperConfig
+    from tw.distill import DistillationTrainer
+    from tw.modeling import WhisperForConditionalGeneration
+    cfg = CONFIGS["micro"]
+    tc = WhisperConfig(**cfg)
+    dev = torch.device("cuda", 0)
+    mk = lambda seed, dt: WhisperForConditionalGeneration.from_state_dict(
+        tc, {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed).items()}, dtype=dt, device=dev)
+    s, t = mk(1, torch.float32), mk(2, torch.bfloat16)
+    tr = DistillationTrainer(s, t, learning_rate=1e-3, gradient_accumulation_steps=2)
+    feats = torch.randn(2, 80, 3000, device=dev)
+    batches = []
+    for seed in (3, 4, 5):
+        dec, lab = L.collate(L.synthetic_label_lists(2, seed=seed, max_len=64))
+        batches.append({"input_features": feats, "decoder_input_ids": torch.from_numpy(dec).to(dev),
+                        "labels": torch.from_numpy(lab).to(dev)})
+    tr.train_step(batches[0])
+    tr.train_step(batches[1])
+    assert tr.step == 1 and tr.micro == 0
+    before = s.store.p32.clone()
+    tr.train_step(batches[2], end_of_dataloader=True)
+    assert tr.step == 2 and tr.micro == 0
+    assert not torch.equal(before, s.store.p32)
