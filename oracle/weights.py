@@ -104,23 +104,44 @@ def param_shapes(cfg: dict) -> dict:
     return s
 
 
-def make_weights(cfg: dict, seed: int, lin_std: float = 0.02) -> dict:
-    """Deterministic HF-keyed float32 state dict (numpy). proj_out is tied, not listed."""
-    rng = np.random.Generator(np.random.PCG64(seed))
-    out = {}
-    for k in sorted(param_shapes(cfg)):
-        shp = param_shapes(cfg)[k]
-        z = rng.standard_normal(shp)
+def _scale(k, z, lin_std, embed_std=0.25):
+    if "layer_norm" in k:
+        w = 1.0 + 0.1 * z if k.endswith("weight") else 0.02 * z
+    elif k.endswith("embed_tokens.weight"):
+        w = embed_std * z
+    elif k.endswith("embed_positions.weight"):
+        w = 0.02 * z
+    else:
+        w = lin_std * z
+    return w.astype(np.float32)
+
+
+def make_weights(cfg: dict, seed: int, lin_std: float = 0.02, per_tensor: bool = False, embed_std: float = 0.25) -> dict:
+    """Deterministic HF-keyed float32 state dict (numpy). proj_out is tied, not listed.
+
+    per_tensor=False: one PCG64(seed) stream over the sorted keys (the micro / tiny fixtures).
+    per_tensor=True (the BASELINE-size fixtures, large-v2 has 1.5 G weights): tensor i of the sorted
+    keys draws from its own PCG64([seed, i]) stream, so the tensors are generated in parallel
+    threads (numpy releases the GIL while filling) with the same values on any machine.
+    embed_std: std of decoder.embed_tokens (0.25 makes the micro config's softmax peaky; at real widths
+    it makes every position predict its own input token, so the BASELINE-size fixtures use 0.05)."""
+    shapes = param_shapes(cfg)
+    keys = sorted(shapes)
+    if not per_tensor:
+        rng = np.random.Generator(np.random.PCG64(seed))
+        out = {}
+        for k in keys:
+            z = rng.standard_normal(shapes[k])
+            out[k] = sinusoids(*shapes[k]) if k.endswith("encoder.embed_positions.weight") else \
+                _scale(k, z, lin_std, embed_std)
+        return out
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(i):
+        k = keys[i]
         if k.endswith("encoder.embed_positions.weight"):
-            out[k] = sinusoids(*shp)
-            continue
-        if "layer_norm" in k:
-            w = 1.0 + 0.1 * z if k.endswith("weight") else 0.02 * z
-        elif k.endswith("embed_tokens.weight"):
-            w = 0.25 * z
-        elif k.endswith("embed_positions.weight"):
-            w = 0.02 * z
-        else:
-            w = lin_std * z
-        out[k] = w.astype(np.float32)
-    return out
+            return k, sinusoids(*shapes[k])
+        z = np.random.Generator(np.random.PCG64([seed, i])).standard_normal(shapes[k])
+        return k, _scale(k, z, lin_std, embed_std)
+    with ThreadPoolExecutor(max_workers=min(16, len(keys))) as ex:
+        return dict(ex.map(one, range(len(keys))))

@@ -283,11 +283,142 @@ def gen_fallback(out):
     out["fb_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
 
 
+# ------------------------------------------------------------------------------------------------
+# BASELINE-config parity fixtures (c1 / c2 / c3 dims).  The reference path is HF Whisper under
+# bf16 autocast (run_distillation.py:815-830 mixed_precision="bf16"; accelerate wraps every prepared
+# model's forward in autocast and upcasts its outputs to fp32, ACC accelerator.py:1818-1829), run here
+# with torch.autocast("cpu", bfloat16): the same op policy for this model (Linear / Conv1d / SDPA in
+# bf16 with fp32 accumulation, cross-entropy in fp32, LayerNorm statistics in fp32 -- CPU autocast
+# returns LN of a bf16 stream in bf16 where CUDA returns fp32, identical once the next Linear casts
+# it), the teacher's weights in bf16 (teacher_dtype, :1011-1018).  The fp32 model (mixed_precision
+# "no") is stored beside it.
+EMBED_STD = 0.05
+CFG_CASES = {
+    # c1: tiny <- tiny, B 2, launcher flags (freeze_encoder -> shared encoder, frozen decoder positions)
+    "c1": dict(student="tiny", teacher="tiny", s_seed=31, t_seed=32, B=2, freeze_encoder=True,
+               freeze_embed_positions=True, label_seed=41, secs=[30.0, 17.0]),
+    # c2: small <- large-v2 (d 768 vs 1280: no sharing, full teacher forward), every student weight
+    # trainable incl. the conv stem and encoder (240.6 M trainable)
+    "c2": dict(student="small", teacher="large-v2", s_seed=33, t_seed=34, B=1, freeze_encoder=False,
+               freeze_embed_positions=False, label_seed=42, secs=[30.0]),
+    # c3: distil-32-2 made by create_student_model from the large-v2 teacher (decoder layers 0 and 31),
+    # frozen shared encoder, a <|startofprev|> prompt (A7 teacher-input quirk at full size)
+    "c3": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=1, freeze_encoder=True,
+               freeze_embed_positions=True, label_seed=43, secs=[30.0], prompt=True),
+}
+
+
+def cfg_case_weights(case):
+    """(student cfg, student weights, teacher cfg, teacher weights) of a BASELINE-config case."""
+    from oracle.student_ref import init_student_from_teacher
+    c = CFG_CASES[case]
+    tcfg = CONFIGS[c["teacher"]]
+    wt = make_weights(tcfg, c["t_seed"], per_tensor=True, embed_std=EMBED_STD)
+    if c["student"] is None:
+        scfg, ws, _, _ = init_student_from_teacher(tcfg, wt, decoder_layers=2)
+    else:
+        scfg = CONFIGS[c["student"]]
+        ws = make_weights(scfg, c["s_seed"], per_tensor=True, embed_std=EMBED_STD)
+    return scfg, ws, tcfg, wt
+
+
+def cfg_case_batch(case):
+    c = CFG_CASES[case]
+    feats = logmel.log_mel_batch([logmel.synthetic_clip(i, c["secs"][i]) for i in range(c["B"])])
+    lists = L.synthetic_label_lists(c["B"], seed=c["label_seed"], prompt_fraction=0.0)
+    if c.get("prompt"):
+        lists[0] = [SPECIAL["startofprev"]] + list(range(300, 340)) + lists[0][:300]
+    dec, lab = L.collate(lists)
+    return feats, dec, lab
+
+
+def _trainable(names, freeze_encoder, freeze_embed_positions):
+    out = []
+    for n in names:
+        if n == "model.encoder.embed_positions.weight":
+            continue
+        if freeze_encoder and n.startswith("model.encoder."):
+            continue
+        if freeze_embed_positions and n == "model.decoder.embed_positions.weight":
+            continue
+        out.append(n)
+    return out
+
+
+def run_hf_step(S, T, feats, dec, lab, share, amp, temperature=2.0):
+    """The reference train_step (run_distillation.py:1519-1551) on HF modules; returns scalars, the
+    fp32 (upcast) logits and the encoder output; gradients land on S's parameters."""
+    import contextlib
+    from transformers.modeling_outputs import BaseModelOutput
+    ctx = (lambda: torch.autocast("cpu", dtype=torch.bfloat16)) if amp else contextlib.nullcontext
+    with ctx():
+        so = S(input_features=feats, decoder_input_ids=dec, labels=lab)
+    s_logits = so.logits.float()
+    enc = so.encoder_last_hidden_state
+    with torch.no_grad(), ctx():
+        if share:
+            to = T(encoder_outputs=BaseModelOutput(enc.detach().to(T.dtype)), labels=lab)
+        else:
+            to = T(input_features=feats, decoder_input_ids=dec, labels=lab)
+    t_logits = to.logits.float()
+    ce = so.loss.float()
+    p = torch.softmax(t_logits / temperature, -1)
+    lq = torch.log_softmax(s_logits / temperature, -1)
+    mask = (lab >= 0).unsqueeze(-1)
+    kl = (torch.nn.functional.kl_div(lq, p, reduction="none") * mask).sum() / mask.sum() * temperature ** 2
+    loss = 0.8 * ce + kl
+    loss.backward()
+    return dict(loss=loss.detach(), ce=ce.detach(), kl=kl.detach(), s_logits=s_logits.detach(),
+                t_logits=t_logits.detach(), enc=enc.detach().float())
+
+
+def gen_cfg(case, out):
+    import time
+    c = CFG_CASES[case]
+    t0 = time.time()
+    scfg, ws, tcfg, wt = cfg_case_weights(case)
+    feats, dec, lab = cfg_case_batch(case)
+    ft, dt, lt = torch.from_numpy(feats), torch.from_numpy(dec), torch.from_numpy(lab)
+    share = c["freeze_encoder"] and scfg["d_model"] == tcfg["d_model"]
+    out["dec"], out["lab"] = dec, lab
+    out["share"] = np.array(share)
+    print(case, "weights", round(time.time() - t0, 1), "s")
+    for mode in ("f32", "amp"):
+        S = hf_model(scfg, ws).train()
+        T = hf_model(tcfg, wt, torch.bfloat16 if mode == "amp" else torch.float32).eval()
+        names = [n for n, _ in S.named_parameters()]
+        tr = _trainable(names, c["freeze_encoder"], c["freeze_embed_positions"])
+        for n, p_ in S.named_parameters():
+            p_.requires_grad_(n in tr)
+        r = run_hf_step(S, T, ft, dt, lt, share, amp=(mode == "amp"))
+        out[f"{mode}|loss"], out[f"{mode}|ce"], out[f"{mode}|kl"] = (np.float64(r[k].item())
+                                                                     for k in ("loss", "ce", "kl"))
+        out[f"{mode}|s_lse"] = torch.logsumexp(r["s_logits"], -1).numpy()
+        out[f"{mode}|t_lse"] = torch.logsumexp(r["t_logits"], -1).numpy()
+        out[f"{mode}|s_argmax"] = r["s_logits"].argmax(-1).numpy()
+        out[f"{mode}|s_rows"] = r["s_logits"][:, ROWS, ::VSTRIDE].numpy()
+        out[f"{mode}|enc_sub"] = r["enc"][:, ::50, :].numpy()
+        out["grad_names"] = np.array(tr)
+        out[f"{mode}|grad_norms"] = np.array([S.get_parameter(n).grad.double().norm().item() for n in tr])
+        p0 = "model.decoder.layers.0.fc1.weight"
+        out[f"{mode}|grad_dec0_fc1_sub"] = S.get_parameter(p0).grad[::37, ::29].clone().numpy()
+        # clip + AdamW (lr 1e-4) as the sync micro-step applies them
+        tp = [S.get_parameter(n) for n in tr]
+        gn = torch.nn.utils.clip_grad_norm_(tp, 1.0)
+        torch.optim.AdamW(tp, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0).step()
+        out[f"{mode}|grad_total_norm"] = np.float64(gn.item())
+        out[f"{mode}|upd_dec0_fc1_sub"] = S.get_parameter(p0).detach()[::37, ::29].clone().numpy()
+        print(case, mode, {k: float(r[k]) for k in ("loss", "ce", "kl")}, round(time.time() - t0, 1), "s")
+        del S, T, r
+
+
 def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
     for name, fn in (("mel", gen_mel), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
-                     ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback)):
+                     ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback),
+                     ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
+                     ("cfg_c3", lambda o: gen_cfg("c3", o))):
         if only and name not in only:
             continue
         out = {}
