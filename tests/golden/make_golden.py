@@ -130,6 +130,14 @@ def gen_micro(out):
     out["grad_total_norm"] = np.float64(gn.item())
     out["upd_dec0_q_sub"] = S.model.decoder.layers[0].self_attn.q_proj.weight.detach()[::5, ::5].numpy()
     out["upd_embed_row"] = S.model.decoder.embed_tokens.weight.detach()[[50260, 100]].numpy()
+    # the same student forward under bf16 autocast (the reference's mixed_precision="bf16" path, see
+    # gen_cfg): the size of the reference's own bf16 noise on this model
+    S2 = hf_model(cfg, ws).eval()
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+        so2 = S2(input_features=feats_t, decoder_input_ids=dec_t, labels=lab_t)
+    out["amp_ce"] = np.float64(so2.loss.float().item())
+    out["amp_enc_sub"] = so2.encoder_last_hidden_state.float().numpy()[:, ::50, :]
+    out["amp_s_lse"] = torch.logsumexp(so2.logits.float(), -1).numpy()
 
 
 def gen_student(out):

@@ -4,7 +4,12 @@ Oracle = oracle/distill_ref.train_step over oracle/whisper_ref.Ref with amp=True
 reference's train_step under CUDA bf16 autocast with the same rounding points as the HIP path
 (pinned to HF fp32 by tests/test_oracle_golden.py).  Tolerances:
   * loss / ce / kl scalars: 1e-3 relative (north-star fp tolerance);
-  * per-parameter gradients: relative L2 error <= 3e-2 and cosine >= 0.999 (bf16 GEMM outputs and
+  * logsumexp of every logit row: one bf16 ulp of the top logit (2^-7) at worst, 3e-4 mean;
+    encoder output (bf16, vs the reference's fp32 LayerNorm output rounded to bf16): relative L2 within
+    the reference's own autocast-vs-fp32 distance (HF under CPU bf16 autocast vs HF fp32, both in the
+    micro_step fixture);
+  * per-parameter gradients: relative L2 error <= 6e-3 (2e-2 for the one worst tensor, the final LN
+    bias) and cosine >= 0.9999 (bf16 GEMM outputs and
     bf16 flash-attention probabilities round at the same points but accumulate in a different
     order, so individual bf16 elements may differ by one ulp);
   * AdamW-updated parameters: <= 2e-3 relative L2 of the update.
@@ -55,21 +60,38 @@ def test_forward_matches_oracle_and_hf():
         r = ref.forward(feats, dec, lab)
     lse = torch.logsumexp(out.logits.float(), -1).cpu()
     rl = torch.logsumexp(r["logits"], -1)
-    # logits are bf16 values (|l| ~ 30 here): allow a few bf16 ulps (2^-8 relative each)
-    assert ((lse - rl).abs() / rl.abs()).max() < 1e-2
-    assert ((lse - rl).abs() / rl.abs()).mean() < 1e-3
-    assert abs(out.loss.item() - r["loss"].item()) / r["loss"].item() < 1e-3
-    # vs the fp32 HF golden: bf16 autocast changes CE by well under 1 %
-    assert abs(out.loss.item() - float(g["ce"])) / float(g["ce"]) < 1e-2
-    enc = out.encoder_last_hidden_state.float().cpu()
-    assert (enc - r["enc"]).abs().max() < 3e-2 * r["enc"].abs().max()
+    lse_err = float(((lse - rl).abs() / rl.abs()).max())
+    ce_amp = abs(out.loss.item() - r["loss"].item()) / r["loss"].item()
+    ce_f32 = abs(out.loss.item() - float(g["ce"])) / float(g["ce"])
+    lse_mean = float(((lse - rl).abs() / rl.abs()).mean())
+    ce_hf_amp = abs(out.loss.item() - float(g["amp_ce"])) / float(g["amp_ce"])
+    enc = out.encoder_last_hidden_state.float().cpu()[:, ::50, :]
+    rl2 = lambda a, b: float((torch.as_tensor(a).double() - torch.as_tensor(b).double()).norm()
+                             / torch.as_tensor(b).double().norm())
+    # the engine hands over encoder_last_hidden_state in bf16 (its only consumers -- the cross-attention
+    # K/V projections and the teacher's .to(bf16), run_distillation.py:1532 -- round it to bf16 anyway):
+    # compare with the reference's fp32 LayerNorm output rounded the same way
+    b16 = lambda a: torch.as_tensor(a).to(torch.bfloat16).float()
+    enc_hf_amp, enc_oracle = rl2(enc, b16(g["amp_enc_sub"])), rl2(enc, b16(r["enc"][:, ::50, :]))
+    # the reference's own bf16 noise on this micro model: HF under autocast vs HF fp32
+    enc_noise = rl2(g["amp_enc_sub"], g["enc_sub"])
+    print(f"micro fwd: lse max rel {lse_err:.2e} mean {lse_mean:.2e}  CE vs oracle {ce_amp:.2e} vs HF amp "
+          f"{ce_hf_amp:.2e} vs HF fp32 {ce_f32:.2e}  enc rel-L2 vs HF amp {enc_hf_amp:.2e} vs oracle "
+          f"{enc_oracle:.2e} (reference bf16 noise {enc_noise:.2e})")
+    # logits are bf16 values (|l| ~ 30 here, peaky: logsumexp ~ the top logit): one bf16 ulp of the top
+    # logit (2^-7 relative) at worst, 3e-4 on average (the HF autocast path's own lse distance from fp32
+    # is 3.6e-3 at worst on this model)
+    assert lse_err <= 2 ** -7 and lse_mean < 3e-4
+    assert ce_amp < 1e-3 and ce_hf_amp < 1e-3 and ce_f32 < 1e-3
+    # encoder output (bf16): within the reference's own autocast-vs-fp32 distance
+    assert enc_hf_amp <= enc_noise and enc_oracle <= 0.5 * enc_noise
     # teacher(encoder_outputs=..., labels) path: shift_tokens_right semantics
     from tw.modeling import BaseModelOutput
     to = t(encoder_outputs=BaseModelOutput(out.encoder_last_hidden_state), labels=lab.cuda())
     tref = Ref(cfg, to_torch(wt, torch.bfloat16), amp=True, stream_bf16=True)
     with torch.no_grad():
         tr = tref.forward(enc=r["enc"].to(torch.bfloat16).float(), labels=lab)
-    assert abs(to.loss.item() - tr["loss"].item()) / tr["loss"].item() < 2e-3
+    assert abs(to.loss.item() - tr["loss"].item()) / tr["loss"].item() < 1e-3
 
 
 @pytest.mark.parametrize("freeze_encoder", [True, False])
@@ -104,8 +126,12 @@ def test_train_step_matches_oracle(freeze_encoder):
         cos = torch.nn.functional.cosine_similarity(got.flatten().double(), want.flatten().double(), 0)
         worst.append((float(err), float(cos), n))
     worst.sort(reverse=True)
-    assert worst[0][0] < 3e-2, worst[:3]
-    assert min(w[1] for w in worst) > 0.999, sorted(worst, key=lambda x: x[1])[:3]
+    print("micro grads: worst rel-L2", worst[:3], "min cos", min(w[1] for w in worst))
+    # the decoder's final LayerNorm bias gradient (a column sum of bf16 products with cancellation) is the
+    # least accurate; every other tensor is within 6e-3
+    assert worst[0][0] < 2e-2, worst[:3]
+    assert worst[1][0] < 6e-3, worst[:3]
+    assert min(w[1] for w in worst) > 0.9999, sorted(worst, key=lambda x: x[1])[:3]
     # second micro-step with the same batch -> optimizer update with the accumulated grads
     tr.train_step(batch)        # two halves of the same batch == one full-batch gradient
     check = ("model.decoder.layers.0.fc1.weight", "model.decoder.embed_tokens.weight",

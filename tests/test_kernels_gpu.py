@@ -497,8 +497,16 @@ def test_logmel_matches_oracle():
     conv = torch.full((3, 3002, 80), 9.0, dtype=torch.bfloat16, device=DEV)
     ops.logmel(wav, basis, start, w, mel, conv)
     ref = ol.log_mel_batch(clips)
-    # oracle float64 vs fp32 DFT: 2e-3 abs on O(1) values
-    assert np.abs(mel.cpu().numpy() - ref).max() < 2e-3
+    got = mel.cpu().numpy()
+    # fp32 DFT on exact-fp32 MFMA vs the float64 oracle: 1e-4 abs on O(1) log-mel values (measured
+    # 5.3e-5 on the driver's smoke run)
+    err = np.abs(got - ref).max()
+    # and vs HF WhisperFeatureExtractor itself (tests/golden/mel.npz: clips 0, 1, 3 are these three)
+    from conftest import load_golden
+    hf = load_golden("mel")["mel_sub"][[0, 1, 3]]
+    err_hf = np.abs(got[:, :, ::10] - hf).max()
+    print(f"log-mel max abs err vs oracle {err:.2e}, vs HF {err_hf:.2e}")
+    assert err < 1e-4 and err_hf < 1e-4
     c = conv.float().cpu()
     assert (c[:, 0] == 0).all() and (c[:, 3001] == 0).all()
     assert (c[:, 1:3001].transpose(1, 2) - bf(mel.cpu()).float()).abs().max() == 0

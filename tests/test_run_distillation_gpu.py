@@ -75,7 +75,7 @@ def test_feed_batches_match_host_path(tmp_path):
     assert idx == [2, 3]                                       # rank 1 takes global micro-batch 1
     wavs = [ds[i]["audio"]["array"].astype(np.float32) for i in idx]
     ref = torch.from_numpy(logmel.log_mel_batch(wavs))
-    assert float((batch["input_features"].cpu() - ref).abs().max()) < 2e-3
+    assert float((batch["input_features"].cpu() - ref).abs().max()) < 2e-4
     assert batch["conv_input"].shape == (2, 3002, 80) and batch["labels"].shape == (2, 447)
     # labels: no prompt (p=0), timestamps kept (p=1): the transcript's ids, shifted, -100 padded
     ids = tok(ds[2]["whisper_transcript"], add_special_tokens=False).input_ids
