@@ -69,10 +69,11 @@ int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const vo
                 float scale, float* workspace /* B*H*Tq floats */, tw_stream_t stream);
 
 /* Fused CE + temperature KL loss and its logits gradient (replaces run_distillation.py:1507-1516,
- * :1539-1549 and HF CE :1082-1087).  out3 = [loss, ce, kl*T^2]; dlogits may be NULL. */
-int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, const int64_t* labels, int64_t rows, int V,
-             float T, float ce_w, float kl_w, const int* n_valid, float grad_scale, float* row_out, float* out3,
-             void* dlogits, tw_stream_t stream);
+ * :1539-1549 and HF CE :1082-1087).  out3 = [loss, ce, kl*T^2]; dlogits (same dtype as the logits:
+ * bf16 under autocast, fp32 on the fp32 path) may be NULL. */
+int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, int logits_dtype, const int64_t* labels,
+             int64_t rows, int V, float T, float ce_w, float kl_w, const int* n_valid, float grad_scale, float* row_out,
+             float* out3, void* dlogits, tw_stream_t stream);
 
 /* Whisper log-mel (replaces WhisperFeatureExtractor at run_distillation.py:1217).
  * wav [B][480000] fp32 -> mel_out [B][80][3000] fp32 and optional conv1 input [B][3002][80] bf16. */
@@ -125,11 +126,14 @@ int tw_count_valid(const int64_t* labels, int64_t n, int* out, tw_stream_t strea
  * next_ids[b], and done[b] |= (token == eos).  With t_dev != NULL: col += *t_dev and the begin mask
  * applies when col == begin_col (apply_begin is ignored).
  * tw_embed_step: out[b] = tok[ids[b]] + pos[*t_dev] (decoder input embedding of one step).
- * tw_kv_append: cache[b*sb + (*t_dev)*ld_row + 0..n) = src[b*ld_src + 0..n) (bf16, n % 8 == 0). */
+ * tw_kv_append: cache[b*sb + (*t_dev)*ld_row + 0..n) = src[b*ld_src + 0..n) (16-B vectors: bf16 n % 8 == 0,
+ * fp32 n % 4 == 0).
+ * dtype / logits_dtype (0 = fp32, 1 = bf16) select the element type of q/K/V/O and of the logits rows:
+ * bf16 under autocast, fp32 on the fp32 path (mixed_precision "no"). */
 int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v, int64_t ldv,
                    int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev, int head_dim,
-                   float scale, tw_stream_t stream);
-int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+                   float scale, int dtype, tw_stream_t stream);
+int tw_greedy_select(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                      const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
                      int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col, tw_stream_t stream);
 /* tw_greedy_select_ts: as tw_greedy_select plus HF WhisperTimeStampLogitsProcessor (applied after the
@@ -138,7 +142,7 @@ int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_
  * -1 = none; updated here), the window's first step limited to timestamps <= ts_begin + max_initial
  * (max_initial < 0: no limit), and timestamps forced when logsumexp over them exceeds the best text
  * logit.  col += *t_dev when t_dev != NULL. */
-int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+int tw_greedy_select_ts(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                         const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids, int col,
                         int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin, int no_ts, int max_initial,
                         int* last_ts, tw_stream_t stream);
@@ -151,20 +155,50 @@ int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint
  * included).  B, V < 2^21.
  * tw_token_logprob: out[b] = log_softmax(logits[b*ld + 0..V))[token] (the no-speech probability is
  * exp(out) at the <|startoftranscript|> position). */
-int tw_select_sample(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+int tw_select_sample(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                      const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
                      int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col, const uint32_t* ctl,
                      float* sum_logp, tw_stream_t stream);
-int tw_select_sample_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+int tw_select_sample_ts(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                         const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids, int col,
                         int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin, int no_ts, int max_initial,
                         int* last_ts, const uint32_t* ctl, float* sum_logp, tw_stream_t stream);
-int tw_token_logprob(const void* logits, int64_t ld, int B, int V, int token, float* out, tw_stream_t stream);
+int tw_token_logprob(const void* logits, int64_t ld, int logits_dtype, int B, int V, int token, float* out,
+                     tw_stream_t stream);
 int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
                   int out_dtype, int B, int D, const int* t_dev, tw_stream_t stream);
-int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n,
+int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n, int dtype,
                  const int* t_dev, tw_stream_t stream);
 int tw_step_advance(int* t_dev, int by, tw_stream_t stream);
+
+/* ---- fp32 arithmetic path (mixed_precision = "no", run_distillation.py:815-823: the reference's default
+ * --dtype float32; the fp32 greedy decode pinned token-for-token to HF fp32 generate).  Exact-fp32 MFMA
+ * (v_mfma_f32_16x16x4_f32), nothing rounded to bf16.
+ * tw_gemm_f32: C[b] = epi(alpha * op(A[b]) op(B[b])^T) with the tw_gemm_bf16 operand conventions
+ *   (A [M][K], a_trans: [K][M]; B [N][K], b_trans: [K][N]) and flags BIAS / GELU (+AUX_OUT) / DGELU / RES /
+ *   ACCUM (ROUND and the tile flags are ignored); bias / res / aux fp32; two batch levels: batch entries
+ *   bz = bo * batch_inner + bi at offsets bo*s? + bi*s?_in.  lda, ldb % 4 == 0, A and B 16-B aligned.
+ * tw_attn_fwd_f32 / tw_attn_bwd_f32: SDPA over (B, H) with head_dim 64 and the tw_attn_* layouts, composed
+ *   from tw_gemm_f32 products and exact row softmax kernels over a caller workspace (fwd >= Tq*round4(Tk)
+ *   floats, bwd twice that; larger workspaces take more (b, h) pairs per pass).  lse [B][H][Tq] (natural log).
+ * tw_mel_to_conv_input_f32 / tw_im2col3_f32 / tw_gelu_bwd_f32: the conv-stem helpers in fp32. */
+int tw_gemm_f32(const float* A, int64_t lda, int a_trans, const float* B, int64_t ldb, int b_trans, float* C,
+                int64_t ldc, int M, int N, int K, int batch, int64_t sA, int64_t sB, int64_t sC, int batch_inner,
+                int64_t sA_in, int64_t sB_in, int64_t sC_in, float alpha, const float* bias, const float* res,
+                int64_t ldr, int64_t sR, int res_mod, float* aux, int64_t ldaux, int64_t sAux, int flags,
+                tw_stream_t stream);
+int tw_attn_fwd_f32(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv, float* O,
+                    int64_t ldo, float* lse, int B, int H, int Tq, int Tk, int head_dim, int causal, float scale,
+                    float* workspace, int64_t workspace_floats, tw_stream_t stream);
+int tw_attn_bwd_f32(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
+                    const float* O, int64_t ldo, const float* dO, int64_t lddo, const float* lse, float* dQ,
+                    int64_t lddq, float* dK, int64_t lddk, float* dV, int64_t lddv, int B, int H, int Tq, int Tk,
+                    int head_dim, int causal, float scale, float* workspace, int64_t workspace_floats,
+                    tw_stream_t stream);
+int tw_mel_to_conv_input_f32(const float* mel, float* xt, int B, int nmel, int T, tw_stream_t stream);
+int tw_im2col3_f32(const float* src, int64_t src_rows, float* dst, int B, int T_out, int stride, int C,
+                   tw_stream_t stream);
+int tw_gelu_bwd_f32(const float* g, const float* pre, float* out, int64_t n, tw_stream_t stream);
 
 #ifdef __cplusplus
 }

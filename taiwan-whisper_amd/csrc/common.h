@@ -30,6 +30,32 @@ __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 __device__ __forceinline__ float rbf(float x) { return (float)(bf16)x; }   // round-trip through bf16 (RNE)
 
+// 8 consecutive elements of a bf16 / fp32 row as fp32 (16-B / 2 x 16-B vector loads; the caller
+// guarantees alignment), and the inverse store
+__device__ __forceinline__ void load8(const bf16* p, float* o) {
+  const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f(v[j]);
+}
+__device__ __forceinline__ void load8(const float* p, float* o) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3]; o[4] = b[0]; o[5] = b[1]; o[6] = b[2]; o[7] = b[3];
+}
+__device__ __forceinline__ void store8(bf16* p, const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+  *(bf16x8*)p = o;
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ float to_f32(bf16 x) { return bf2f(x); }
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ void from_f32(bf16& d, float x) { d = f2bf(x); }
+__device__ __forceinline__ void from_f32(float& d, float x) { d = x; }
+
 __device__ __forceinline__ float ld_as_f32(const void* p, int dtype, int64_t i) {
   return dtype == TW_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
 }

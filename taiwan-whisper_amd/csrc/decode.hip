@@ -28,16 +28,18 @@ constexpr int DA_THREADS = 256;
 constexpr int DA_MAX_TK = 2048;
 
 struct DecP {
-  const bf16* q; int64_t sqb;
-  const bf16* k; int64_t ldk, skb;
-  const bf16* v; int64_t ldv, svb;
-  bf16* o; int64_t sob;
+  const void* q; int64_t sqb;
+  const void* k; int64_t ldk, skb;
+  const void* v; int64_t ldv, svb;
+  void* o; int64_t sob;
   int H, Tk;
   const int* tk_dev;  // nullable: effective Tk = *tk_dev + Tk (graph-captured decode steps)
   float c;        // scale * log2(e)
 };
 
-// lane = (key slot ks = lane >> 3, 16-B chunk ch = lane & 7); a wave covers 8 keys per step
+// lane = (key slot ks = lane >> 3, 8-element chunk ch = lane & 7); a wave covers 8 keys per step.
+// E = bf16 (autocast path) or float (fp32 path: exact expf, no rounding of the output)
+template <typename E>
 __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
   __shared__ float sc[DA_MAX_TK];
   __shared__ float red[DA_THREADS / 64][64];
@@ -48,24 +50,22 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
   if (p.tk_dev) p.Tk += *p.tk_dev;
   if (p.Tk > DA_MAX_TK) p.Tk = DA_MAX_TK;
-  const bf16* qb = p.q + b * p.sqb + h * 64 + ch * 8;
-  const bf16* kb = p.k + b * p.skb + h * 64 + ch * 8;
-  const bf16* vb = p.v + b * p.svb + h * 64 + ch * 8;
+  constexpr bool F32 = sizeof(E) == 4;
+  const E* qb = (const E*)p.q + b * p.sqb + h * 64 + ch * 8;
+  const E* kb = (const E*)p.k + b * p.skb + h * 64 + ch * 8;
+  const E* vb = (const E*)p.v + b * p.svb + h * 64 + ch * 8;
   float qv[8];
-  {
-    const bf16x8 t = *(const bf16x8*)qb;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qv[j] = bf2f(t[j]);
-  }
+  load8(qb, qv);
   // pass 1: scores (log2 domain) -> LDS, running max
   float mx = -INFINITY;
   for (int k0 = wave * 8; k0 < p.Tk; k0 += DA_THREADS / 8) {
     const int key = k0 + ks;
     float s = 0.f;
     if (key < p.Tk) {
-      const bf16x8 t = *(const bf16x8*)(kb + (int64_t)key * p.ldk);
+      float t[8];
+      load8(kb + (int64_t)key * p.ldk, t);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s = fmaf(qv[j], bf2f(t[j]), s);
+      for (int j = 0; j < 8; ++j) s = fmaf(qv[j], t[j], s);
     }
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
@@ -88,10 +88,11 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
   for (int k0 = wave * 8; k0 < p.Tk; k0 += DA_THREADS / 8) {
     const int key = k0 + ks;
     if (key < p.Tk) {
-      const float pe = __builtin_amdgcn_exp2f(sc[key] - m);
-      const bf16x8 t = *(const bf16x8*)(vb + (int64_t)key * p.ldv);
+      const float pe = F32 ? exp2f(sc[key] - m) : __builtin_amdgcn_exp2f(sc[key] - m);
+      float t[8];
+      load8(vb + (int64_t)key * p.ldv, t);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fmaf(pe, bf2f(t[j]), o[j]);
+      for (int j = 0; j < 8; ++j) o[j] = fmaf(pe, t[j], o[j]);
       if (ch == 0) l += pe;
     }
   }
@@ -116,12 +117,12 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
       acc += red[w][tid];
       lt += red_l[w];
     }
-    p.o[b * p.sob + h * 64 + tid] = f2bf(acc / lt);
+    from_f32(((E*)p.o)[b * p.sob + h * 64 + tid], acc / lt);
   }
 }
 
 struct SelP {
-  const bf16* logits; int64_t ld;
+  const void* logits; int64_t ld;
   int V;
   const uint32_t* suppress;   // V-bit mask (nullable)
   const uint32_t* begin;      // V-bit mask applied when apply_begin (nullable)
@@ -139,17 +140,15 @@ struct SelP {
 
 // f(v, x, suppressed, begin_suppressed) over this thread's ids of a logits row: chunks of 8
 // consecutive ids (one 16-B load, one word of each mask), chunk c = tid, tid + 256, ...
-template <class F>
-__device__ __forceinline__ void for_row(const SelP& p, const bf16* row, F&& f) {
+template <typename E, class F>
+__device__ __forceinline__ void for_row(const SelP& p, const E* row, F&& f) {
   for (int v0 = (int)threadIdx.x * 8; v0 < p.V; v0 += 256 * 8) {
     float xs[8];
     if (p.vec) {
-      const bf16x8 t = *(const bf16x8*)(row + v0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xs[j] = bf2f(t[j]);
+      load8(row + v0, xs);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xs[j] = v0 + j < p.V ? bf2f(row[v0 + j]) : -INFINITY;
+      for (int j = 0; j < 8; ++j) xs[j] = v0 + j < p.V ? to_f32(row[v0 + j]) : -INFINITY;
     }
     const uint32_t ws = p.suppress ? p.suppress[v0 >> 5] >> (v0 & 31) : 0u;   // 8 ids never straddle a word
     const uint32_t wb = p.begin ? p.begin[v0 >> 5] >> (v0 & 31) : 0u;
@@ -215,6 +214,7 @@ __device__ __forceinline__ void block_lse(float& m, float& s, float (*sv)[4], in
 
 __device__ __forceinline__ bool bit(const uint32_t* m, int v) { return m && ((m[v >> 5] >> (v & 31)) & 1u); }
 
+template <typename E>
 __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
   __shared__ float sv[4][4];
   __shared__ int si[4][4];
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
   uint64_t seed;
   read_ctl(p.ctl, inv_t, seed);
   const bool sample = inv_t > 0.f;
-  const bf16* row = p.logits + b * p.ld;
+  const E* row = (const E*)p.logits + b * p.ld;
   float best = -INFINITY, sbest = -INFINITY, m = -INFINITY, se = 0.f;
   int besti = 0x7fffffff, sbesti = 0x7fffffff;
   for_row(p, row, [&](int v, float x, bool sup, bool beg) {
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
     p.ids[b * p.ld_ids + p.col] = tok;
     p.next[b] = tok;
     p.done[b] = (fin || tok == p.eos) ? 1 : 0;
-    if (p.sum_logp && !fin) p.sum_logp[b] += bf2f(row[pick]) - lse_val(m, se);
+    if (p.sum_logp && !fin) p.sum_logp[b] += to_f32(row[pick]) - lse_val(m, se);
   }
 }
 
@@ -272,6 +272,7 @@ struct SelTsP {
   int* last_ts;
 };
 
+template <typename E>
 __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   __shared__ float sv[4][3];
   __shared__ int si[4][2];
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   const int lt = q.last_ts[b];
   const int lim = lt < 0 ? q.ts_begin : ((last_ts && !pen_ts) ? lt : lt + 1);
   const int ts_hi = (first && q.max_initial >= 0) ? q.ts_begin + q.max_initial : 0x7fffffff;
-  const bf16* row = p.logits + b * p.ld;
+  const E* row = (const E*)p.logits + b * p.ld;
   // eligibility of id v before the "timestamp mass wins" rule
   auto masked = [&](int v, bool sup, bool beg) -> bool {
     bool m = sup || (first && beg) || v == q.no_ts;
@@ -389,24 +390,25 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
         if (bs > -INFINITY) lse_merge(m, ss, bs, sv[0][2]);
         lse = lse_val(m, ss);
       }
-      p.sum_logp[b] += bf2f(row[best]) - lse;
+      p.sum_logp[b] += to_f32(row[best]) - lse;
     }
   }
 }
 
-// out[b] = log_softmax(logits[b, :V])[token]   (fp32 of the bf16 row)
-__global__ __launch_bounds__(256) void token_logprob_kernel(const bf16* __restrict__ logits, int64_t ld, int V,
+// out[b] = log_softmax(logits[b, :V])[token]   (fp32 of the bf16 / fp32 row)
+template <typename E>
+__global__ __launch_bounds__(256) void token_logprob_kernel(const E* __restrict__ logits, int64_t ld, int V,
                                                             int token, float* __restrict__ out) {
   __shared__ float sv[4][4];
   const int b = blockIdx.x;
-  const bf16* row = logits + b * ld;
+  const E* row = logits + b * ld;
   float m = -INFINITY, s = 0.f;
   for (int v = threadIdx.x; v < V; v += 256) {
-    const float x = bf2f(row[v]);
+    const float x = to_f32(row[v]);
     if (x > -INFINITY) lse_add(m, s, x);
   }
   block_lse(m, s, sv, 0);
-  if (threadIdx.x == 0) out[b] = bf2f(row[token]) - lse_val(m, s);
+  if (threadIdx.x == 0) out[b] = to_f32(row[token]) - lse_val(m, s);
 }
 
 // x[b] = tok[ids[b]] + pos[*t_dev]   (decoder input embedding of step t, HF modeling_whisper.py:720-735)
@@ -423,45 +425,55 @@ __global__ void embed_step_kernel(const int64_t* __restrict__ ids, const void* _
   }
 }
 
-// cache[b][*t_dev][0:n] = src[b][0:n]   (16-B vectors)
-__global__ void kv_append_kernel(const bf16* __restrict__ src, int64_t ld_src, bf16* __restrict__ cache,
+// cache[b][*t_dev][0:n] = src[b][0:n]   (16-B vectors: 8 bf16 or 4 fp32)
+template <typename E>
+__global__ void kv_append_kernel(const E* __restrict__ src, int64_t ld_src, E* __restrict__ cache,
                                  int64_t ld_row, int64_t sb, int n, const int* __restrict__ t_dev) {
+  constexpr int W = 16 / sizeof(E);
   const int b = blockIdx.y;
   const int64_t t = *t_dev;
-  const int i = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (i < n) *(bf16x8*)(cache + b * sb + t * ld_row + i) = *(const bf16x8*)(src + b * ld_src + i);
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) * W;
+  if (i < n) *(f32x4*)(cache + b * sb + t * ld_row + i) = *(const f32x4*)(src + b * ld_src + i);
 }
 
 __global__ void step_advance_kernel(int* t_dev, int by) {
   if (threadIdx.x == 0) *t_dev += by;
 }
 
-// 16-B row loads when every row starts 16-B aligned and has room for the last 8-id chunk
+// vector row loads when every row starts 16-B aligned and has room for the last 8-id chunk
 int sel_vec(const void* logits, int64_t ld, int V) {
   return ((uintptr_t)logits % 16 == 0 && ld % 8 == 0 && ld >= (int64_t)((V + 7) / 8) * 8) ? 1 : 0;
 }
 
+// launch K<bf16> or K<float> by the logits dtype code
+#define TW_LAUNCH_DT(dt, K, grid, block, ...)                                              \
+  do {                                                                                      \
+    if ((dt) == TW_BF16) hipLaunchKernelGGL(K<bf16>, grid, block, 0, stream, __VA_ARGS__);   \
+    else if ((dt) == TW_F32) hipLaunchKernelGGL(K<float>, grid, block, 0, stream, __VA_ARGS__); \
+    else return TW_EUNSUPPORTED;                                                            \
+  } while (0)
+
 }  // namespace
 
-extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                                    const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids,
                                    int col, int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin,
                                    int no_ts, int max_initial, int* last_ts, hipStream_t stream) {
   if (B <= 0) return TW_OK;
   if (V <= 0 || ld < V || !done || !ids || !next_ids || !last_ts || ts_begin <= eos || ts_begin > V) return TW_EINVAL;
   SelTsP q;
-  q.s.logits = (const bf16*)logits; q.s.ld = ld; q.s.V = V;
+  q.s.logits = logits; q.s.ld = ld; q.s.V = V;
   q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
   q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
   q.s.ctl = nullptr; q.s.sum_logp = nullptr; q.s.vec = sel_vec(logits, ld, V);
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
-  hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
+  TW_LAUNCH_DT(logits_dtype, greedy_select_ts_kernel, dim3(B), dim3(256), q);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
 
-extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                                    const uint32_t* begin_bits, int64_t eos, uint8_t* done, int64_t* ids, int64_t ld_ids,
                                    int col, int64_t* next_ids, const int* t_dev, int begin_col, int ts_begin,
                                    int no_ts, int max_initial, int* last_ts, const uint32_t* ctl, float* sum_logp,
@@ -470,22 +482,28 @@ extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int B, int V,
   if (V <= 0 || ld < V || !done || !ids || !next_ids || !last_ts || ts_begin <= eos || ts_begin > V) return TW_EINVAL;
   if (B >= (1 << 21) || V >= (1 << 21)) return TW_EUNSUPPORTED;     // RNG key widths
   SelTsP q;
-  q.s.logits = (const bf16*)logits; q.s.ld = ld; q.s.V = V;
+  q.s.logits = logits; q.s.ld = ld; q.s.V = V;
   q.s.suppress = suppress_bits; q.s.begin = begin_bits; q.s.apply_begin = 0;
   q.s.eos = eos; q.s.done = done; q.s.ids = ids; q.s.ld_ids = ld_ids; q.s.col = col; q.s.next = next_ids;
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
   q.s.ctl = ctl; q.s.sum_logp = sum_logp; q.s.vec = sel_vec(logits, ld, V);
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
-  hipLaunchKernelGGL(greedy_select_ts_kernel, dim3(B), dim3(256), 0, stream, q);
+  TW_LAUNCH_DT(logits_dtype, greedy_select_ts_kernel, dim3(B), dim3(256), q);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
 
-extern "C" int tw_token_logprob(const void* logits, int64_t ld, int B, int V, int token, float* out,
-                                hipStream_t stream) {
+extern "C" int tw_token_logprob(const void* logits, int64_t ld, int logits_dtype, int B, int V, int token,
+                                float* out, hipStream_t stream) {
   if (B <= 0) return TW_OK;
   if (V <= 0 || ld < V || token < 0 || token >= V || !out) return TW_EINVAL;
-  hipLaunchKernelGGL(token_logprob_kernel, dim3(B), dim3(256), 0, stream, (const bf16*)logits, ld, V, token, out);
+  if (logits_dtype == TW_BF16)
+    hipLaunchKernelGGL(token_logprob_kernel<bf16>, dim3(B), dim3(256), 0, stream, (const bf16*)logits, ld, V, token, out);
+  else if (logits_dtype == TW_F32)
+    hipLaunchKernelGGL(token_logprob_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)logits, ld, V, token,
+                       out);
+  else
+    return TW_EUNSUPPORTED;
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
@@ -501,12 +519,19 @@ extern "C" int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype,
 }
 
 extern "C" int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n,
-                            const int* t_dev, hipStream_t stream) {
+                            int dtype, const int* t_dev, hipStream_t stream) {
   if (B <= 0 || n <= 0) return TW_OK;
-  if (!t_dev || (n & 7) || (ld_src & 7) || (ld_row & 7) || (sb & 7) || (((uintptr_t)src | (uintptr_t)cache) & 15))
+  const int w = dtype == TW_F32 ? 3 : 7;          // 16-B vectors: 4 fp32 / 8 bf16
+  if (!t_dev || (n & w) || (ld_src & w) || (ld_row & w) || (sb & w) || (((uintptr_t)src | (uintptr_t)cache) & 15))
     return TW_EINVAL;
-  hipLaunchKernelGGL(kv_append_kernel, dim3((n / 8 + 255) / 256, B), dim3(256), 0, stream, (const bf16*)src, ld_src,
-                     (bf16*)cache, ld_row, sb, n, t_dev);
+  if (dtype == TW_BF16)
+    hipLaunchKernelGGL(kv_append_kernel<bf16>, dim3((n / 8 + 255) / 256, B), dim3(256), 0, stream, (const bf16*)src,
+                       ld_src, (bf16*)cache, ld_row, sb, n, t_dev);
+  else if (dtype == TW_F32)
+    hipLaunchKernelGGL(kv_append_kernel<float>, dim3((n / 4 + 255) / 256, B), dim3(256), 0, stream, (const float*)src,
+                       ld_src, (float*)cache, ld_row, sb, n, t_dev);
+  else
+    return TW_EUNSUPPORTED;
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
@@ -520,41 +545,42 @@ extern "C" int tw_step_advance(int* t_dev, int by, hipStream_t stream) {
 
 extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v,
                               int64_t ldv, int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev,
-                              int head_dim, float scale, hipStream_t stream) {
+                              int head_dim, float scale, int dtype, hipStream_t stream) {
   if (head_dim != 64) return TW_EUNSUPPORTED;
   if (B <= 0 || H <= 0) return TW_OK;
   if ((!tk_dev && Tk <= 0) || Tk > DA_MAX_TK) return TW_EUNSUPPORTED;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) return TW_EINVAL;
   if ((sqb | ldk | skb | ldv | svb) & 7) return TW_EINVAL;
   DecP p;
-  p.q = (const bf16*)q; p.sqb = sqb;
-  p.k = (const bf16*)k; p.ldk = ldk; p.skb = skb;
-  p.v = (const bf16*)v; p.ldv = ldv; p.svb = svb;
-  p.o = (bf16*)o; p.sob = sob;
+  if (dtype == TW_F32 && ((sqb | ldk | skb | ldv | svb) & 3)) return TW_EINVAL;
+  p.q = q; p.sqb = sqb;
+  p.k = k; p.ldk = ldk; p.skb = skb;
+  p.v = v; p.ldv = ldv; p.svb = svb;
+  p.o = o; p.sob = sob;
   p.H = H; p.Tk = Tk; p.tk_dev = tk_dev; p.c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(decode_attn_kernel, dim3(B * H), dim3(DA_THREADS), 0, stream, p);
+  TW_LAUNCH_DT(dtype, decode_attn_kernel, dim3(B * H), dim3(DA_THREADS), p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
 
-extern "C" int tw_greedy_select(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+extern "C" int tw_greedy_select(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                                 const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
                                 int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col,
                                 hipStream_t stream) {
   if (B <= 0) return TW_OK;
   if (V <= 0 || ld < V || !done || !ids || !next_ids) return TW_EINVAL;
   SelP p;
-  p.logits = (const bf16*)logits; p.ld = ld; p.V = V;
+  p.logits = logits; p.ld = ld; p.V = V;
   p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
   p.ctl = nullptr; p.sum_logp = nullptr; p.vec = sel_vec(logits, ld, V);
-  hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
+  TW_LAUNCH_DT(logits_dtype, greedy_select_kernel, dim3(B), dim3(256), p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
 
-extern "C" int tw_select_sample(const void* logits, int64_t ld, int B, int V, const uint32_t* suppress_bits,
+extern "C" int tw_select_sample(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                                 const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
                                 int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col,
                                 const uint32_t* ctl, float* sum_logp, hipStream_t stream) {
@@ -562,12 +588,12 @@ extern "C" int tw_select_sample(const void* logits, int64_t ld, int B, int V, co
   if (V <= 0 || ld < V || !done || !ids || !next_ids) return TW_EINVAL;
   if (B >= (1 << 21) || V >= (1 << 21)) return TW_EUNSUPPORTED;     // RNG key widths
   SelP p;
-  p.logits = (const bf16*)logits; p.ld = ld; p.V = V;
+  p.logits = logits; p.ld = ld; p.V = V;
   p.suppress = suppress_bits; p.begin = begin_bits; p.apply_begin = apply_begin;
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
   p.ctl = ctl; p.sum_logp = sum_logp; p.vec = sel_vec(logits, ld, V);
-  hipLaunchKernelGGL(greedy_select_kernel, dim3(B), dim3(256), 0, stream, p);
+  TW_LAUNCH_DT(logits_dtype, greedy_select_kernel, dim3(B), dim3(256), p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

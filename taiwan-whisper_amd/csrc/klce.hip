@@ -1,5 +1,5 @@
 // Fused distillation loss head: for every decoder position with
-// label >= 0, from the bf16 student / teacher logit rows (the reference's fp32 logits are
+// label >= 0, from the student / teacher logit rows (bf16 under autocast, fp32 on the fp32 path) (the reference's fp32 logits are
 // exactly these bf16 values upcast, ACC:accelerator.py:1818-1829):
 //   ce_row = logsumexp(s) - s[label]                                (HF:modeling_whisper.py:1082-1087)
 //   kl_row = sum_v p_v (log p_v - log q_v),  p = softmax(t/T), log q = log_softmax(s/T)
@@ -46,36 +46,39 @@ __device__ __forceinline__ Stats shfl_stats(const Stats& s, int o) {
   return r;
 }
 
-__global__ __launch_bounds__(NT) void klce_kernel(const bf16* __restrict__ S, const bf16* __restrict__ Tl, int64_t ld,
+template <typename E>
+__global__ __launch_bounds__(NT) void klce_kernel(const E* __restrict__ S, const E* __restrict__ Tl, int64_t ld,
                                                   const int64_t* __restrict__ labels, int V, float T, float ce_w,
                                                   float kl_w, const int* __restrict__ n_valid, float grad_scale,
-                                                  float* __restrict__ row_out, bf16* __restrict__ dS) {
+                                                  float* __restrict__ row_out, E* __restrict__ dS) {
   __shared__ Stats red[NT / 64];
   const int64_t row = blockIdx.x;
   const int64_t lab = labels[row];
   const int tid = threadIdx.x;
   const int nch = (V + 7) / 8;          // 8-wide chunks covering [0, V)
   const int nch_ld = (int)(ld / 8);     // chunks covering the padded row
-  const bf16* srow = S + row * ld;
-  const bf16* trow = Tl + row * ld;
+  const E* srow = S + row * ld;
+  const E* trow = Tl + row * ld;
+  const float zero8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (lab < 0) {
     if (tid == 0) { row_out[row * 2] = 0.f; row_out[row * 2 + 1] = 0.f; }
     if (dS)
-      for (int c = tid; c < nch_ld; c += NT) *(bf16x8*)(dS + row * ld + c * 8) = bf16x8{};
+      for (int c = tid; c < nch_ld; c += NT) store8(dS + row * ld + c * 8, zero8);
     return;
   }
   const float invT = 1.f / T;
   Stats st = {-INFINITY, 0.f, 0.f, -INFINITY, 0.f, 0.f};
   for (int c = tid; c < nch; c += NT) {
-    const bf16x8 sv = *(const bf16x8*)(srow + c * 8);
-    const bf16x8 tv = *(const bf16x8*)(trow + c * 8);
+    float sv[8], tv[8];
+    load8(srow + c * 8, sv);
+    load8(trow + c * 8, tv);
     float s[8], t[8];
     float cms = -INFINITY, cmt = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool ok = c * 8 + j < V;
-      s[j] = ok ? bf2f(sv[j]) : -INFINITY;
-      t[j] = ok ? bf2f(tv[j]) : -INFINITY;
+      s[j] = ok ? sv[j] : -INFINITY;
+      t[j] = ok ? tv[j] : -INFINITY;
       cms = fmaxf(cms, s[j]);
       cmt = fmaxf(cmt, t[j]);
     }
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(NT) void klce_kernel(const bf16* __restrict__ S, co
   const float lse1 = tot.ms + __logf(tot.z1);                // logsumexp(s)
   const float lsesT = tot.ms * invT + __logf(tot.zt);        // logsumexp(s/T)
   const float lsetT = tot.mt * invT + __logf(tot.ztt);       // logsumexp(t/T)
-  const float s_lab = bf2f(srow[lab]);
+  const float s_lab = to_f32(srow[lab]);
   if (tid == 0) {
     row_out[row * 2] = lse1 - s_lab;
     row_out[row * 2 + 1] = (tot.a / tot.ztt) * invT - lsetT + lsesT;
@@ -121,26 +124,26 @@ __global__ __launch_bounds__(NT) void klce_kernel(const bf16* __restrict__ S, co
   const float N = (float)max(*n_valid, 1);
   const float gce = grad_scale * ce_w / N;
   const float gkl = grad_scale * kl_w * T / N;
-  bf16* drow = dS + row * ld;
+  E* drow = dS + row * ld;
   for (int c = tid; c < nch_ld; c += NT) {
-    bf16x8 out = bf16x8{};
+    float out[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (c < nch) {
-      const bf16x8 sv = *(const bf16x8*)(srow + c * 8);
-      const bf16x8 tv = *(const bf16x8*)(trow + c * 8);
+      float sv[8], tv[8];
+      load8(srow + c * 8, sv);
+      load8(trow + c * 8, tv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int v = c * 8 + j;
         if (v < V) {
-          const float s = bf2f(sv[j]), t = bf2f(tv[j]);
+          const float s = sv[j], t = tv[j];
           const float sm1 = __expf(s - lse1);
           const float q = __expf(s * invT - lsesT);
           const float pp = __expf(t * invT - lsetT);
-          float gv = gce * (sm1 - (v == lab ? 1.f : 0.f)) + gkl * (q - pp);
-          out[j] = f2bf(gv);
+          out[j] = gce * (sm1 - (v == lab ? 1.f : 0.f)) + gkl * (q - pp);
         }
       }
     }
-    *(bf16x8*)(drow + c * 8) = out;
+    store8(drow + c * 8, out);
   }
 }
 
@@ -166,14 +169,21 @@ __global__ void klce_reduce_kernel(const float* __restrict__ row_out, int64_t ro
 }  // namespace
 
 // row_out: rows*2 floats workspace; out3: [loss, ce, kl]; dlogits may be null (eval / no grad).
-extern "C" int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, const int64_t* labels, int64_t rows,
-                        int V, float T, float ce_w, float kl_w, const int* n_valid, float grad_scale, float* row_out,
-                        float* out3, void* dlogits, hipStream_t stream) {
+extern "C" int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, int logits_dtype,
+                        const int64_t* labels, int64_t rows, int V, float T, float ce_w, float kl_w, const int* n_valid,
+                        float grad_scale, float* row_out, float* out3, void* dlogits, hipStream_t stream) {
   if (rows <= 0) return TW_OK;
   if ((ld % 8) != 0 || ld < V) return TW_EINVAL;
-  if ((((uintptr_t)s_logits) | ((uintptr_t)t_logits)) & 15) return TW_EINVAL;
-  hipLaunchKernelGGL(klce_kernel, dim3(rows), dim3(NT), 0, stream, (const bf16*)s_logits, (const bf16*)t_logits, ld,
-                     labels, V, T, ce_w, kl_w, n_valid, grad_scale, row_out, (bf16*)dlogits);
+  if ((((uintptr_t)s_logits) | ((uintptr_t)t_logits) | ((uintptr_t)dlogits)) & 15) return TW_EINVAL;
+  if (logits_dtype == TW_BF16)
+    hipLaunchKernelGGL(klce_kernel<bf16>, dim3(rows), dim3(NT), 0, stream, (const bf16*)s_logits, (const bf16*)t_logits,
+                       ld, labels, V, T, ce_w, kl_w, n_valid, grad_scale, row_out, (bf16*)dlogits);
+  else if (logits_dtype == TW_F32)
+    hipLaunchKernelGGL(klce_kernel<float>, dim3(rows), dim3(NT), 0, stream, (const float*)s_logits,
+                       (const float*)t_logits, ld, labels, V, T, ce_w, kl_w, n_valid, grad_scale, row_out,
+                       (float*)dlogits);
+  else
+    return TW_EUNSUPPORTED;
   hipLaunchKernelGGL(klce_reduce_kernel, dim3(1), dim3(1024), 0, stream, row_out, rows, n_valid, T, ce_w, kl_w, out3);
   TW_CHECK_LAUNCH();
   return TW_OK;

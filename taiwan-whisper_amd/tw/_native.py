@@ -23,7 +23,7 @@ SIGNATURES = {
     "tw_attn_fwd": [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, F32, P],
     "tw_attn_bwd": [P, I64, P, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, I32, I32, I32, I32,
                     I32, I32, F32, P, P],
-    "tw_kl_ce": [P, P, I64, P, I64, I32, F32, F32, F32, P, F32, P, P, P, P],
+    "tw_kl_ce": [P, P, I64, I32, P, I64, I32, F32, F32, F32, P, F32, P, P, P, P],
     "tw_logmel": [P, I32, P, P, P, P, P, P, P],
     "tw_mel_to_conv_input": [P, P, I32, I32, I32, P],
     "tw_embed_fwd": [P, P, I32, P, I32, P, I32, I32, I32, I32, I32, P],
@@ -38,15 +38,24 @@ SIGNATURES = {
     "tw_gelu_bwd": [P, I32, P, P, I64, P],
     "tw_shift_tokens_right": [P, P, I32, I32, I64, I64, P],
     "tw_count_valid": [P, I64, P, P],
-    "tw_decode_attn": [P, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, I32, P, I32, F32, P],
-    "tw_greedy_select": [P, I64, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P],
-    "tw_greedy_select_ts": [P, I64, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P],
-    "tw_select_sample": [P, I64, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P, P, P],
-    "tw_select_sample_ts": [P, I64, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P, P, P],
-    "tw_token_logprob": [P, I64, I32, I32, I32, P, P],
+    "tw_decode_attn": [P, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, I32, P, I32, F32, I32, P],
+    "tw_greedy_select": [P, I64, I32, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P],
+    "tw_greedy_select_ts": [P, I64, I32, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P],
+    "tw_select_sample": [P, I64, I32, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P, P, P],
+    "tw_select_sample_ts": [P, I64, I32, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P, P, P],
+    "tw_token_logprob": [P, I64, I32, I32, I32, I32, P, P],
     "tw_embed_step": [P, P, I32, P, I32, P, I32, I32, I32, P, P],
-    "tw_kv_append": [P, I64, P, I64, I64, I32, I32, P, P],
+    "tw_kv_append": [P, I64, P, I64, I64, I32, I32, I32, P, P],
     "tw_step_advance": [P, I32, P],
+    # fp32 arithmetic path
+    "tw_gemm_f32": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I64, I64, I64, I32, I64, I64, I64, F32,
+                    P, P, I64, I64, I32, P, I64, I64, I32, P],
+    "tw_attn_fwd_f32": [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, F32, P, I64, P],
+    "tw_attn_bwd_f32": [P, I64, P, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, I32, I32, I32, I32, I32,
+                        I32, F32, P, I64, P],
+    "tw_mel_to_conv_input_f32": [P, P, I32, I32, I32, P],
+    "tw_im2col3_f32": [P, I64, P, I32, I32, I32, I32, P],
+    "tw_gelu_bwd_f32": [P, P, P, I64, P],
 }
 
 STATUS = {1: "invalid argument / shape", 2: "unsupported configuration", 3: "HIP launch error"}

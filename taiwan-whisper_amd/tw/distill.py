@@ -79,6 +79,9 @@ class DistillationTrainer:
                  lr_scheduler_type: str = "constant_with_warmup", max_steps: int = 0,
                  gradient_accumulation_steps: int = 1, freeze_encoder: bool = True, freeze_decoder: bool = False,
                  freeze_embed_positions: bool = True, process_group=None, dp_bucket_mb: int = 64):
+        if student.compute != teacher.compute:
+            raise ValueError(f"student computes in {student.compute}, teacher in {teacher.compute}: the reference "
+                             "runs both under one mixed_precision setting")
         self.s, self.t = student, teacher
         self.temperature, self.kl_weight = temperature, kl_weight
         self.lr, self.b1, self.b2, self.eps = learning_rate, adam_beta1, adam_beta2, adam_epsilon
@@ -122,8 +125,9 @@ class DistillationTrainer:
 
     # ------------------------------------------------------------------ forward pieces
     def _conv_input(self, batch):
-        if batch.get("conv_input") is not None:
-            return batch["conv_input"]
+        ci = batch.get("conv_input")
+        if ci is not None and ci.dtype == self.s.act_dtype:
+            return ci                       # the feed's log-mel kernel emitted it in the compute dtype
         return self.s.conv_input(batch["input_features"])
 
     def _teacher_logits(self, conv_in, ids, labels, enc16, Tk):

@@ -39,20 +39,21 @@ class DecodeSession:
         self.H = self.d // 64
         dev = model.device
         d = self.d
-        self.self_kv = [torch.empty(B, T_max, 2 * d, dtype=torch.bfloat16, device=dev)
+        act = model.act_dtype            # bf16 (autocast) or fp32 (fp32 path): caches, operands, logits
+        self.self_kv = [torch.empty(B, T_max, 2 * d, dtype=act, device=dev)
                         for _ in range(cfg.decoder_layers)]
-        self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=dev)
+        self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
                          for _ in range(cfg.decoder_layers)]
         self.set_encoder(enc16)
         self.t_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cur = torch.zeros(B, dtype=torch.int64, device=dev)       # this step's input ids
         self.x = torch.empty(B, d, dtype=model.stream_dtype, device=dev)
-        self.y = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
-        self.qkv = torch.empty(B, 3 * d, dtype=torch.bfloat16, device=dev)
-        self.o = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
-        self.q = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
-        self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=torch.bfloat16, device=dev)
-        self.logits = torch.empty(B, model.Vp, dtype=torch.bfloat16, device=dev)
+        self.y = torch.empty(B, d, dtype=act, device=dev)
+        self.qkv = torch.empty(B, 3 * d, dtype=act, device=dev)
+        self.o = torch.empty(B, d, dtype=act, device=dev)
+        self.q = torch.empty(B, d, dtype=act, device=dev)
+        self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=act, device=dev)
+        self.logits = torch.empty(B, model.Vp, dtype=act, device=dev)
         self.graph = None
 
     def set_encoder(self, enc16):
@@ -60,8 +61,8 @@ class DecodeSession:
         m, d = self.m, self.d
         for i, kv in enumerate(self.cross_kv):
             p = f"model.decoder.layers.{i}.encoder_attn"
-            wkv = m.store.span(m.store.p16, p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
-            bkv = m.store.span(m.store.p16, p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
+            wkv = m.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
+            bkv = m.wspan(p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
             m._lin(enc16, wkv, bkv, kv)
 
     def _ln(self, x, name):
@@ -84,9 +85,8 @@ class DecodeSession:
             p = f"model.decoder.layers.{i}"
             # self attention: fused QKV -> staging; k, v appended at row t of the cache
             y = self._ln(x, p + ".self_attn_layer_norm")
-            wqkv = m.store.span(m.store.p16, p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight",
-                                (3 * d, d))
-            bqkv = m.store.span(m.store.p16, p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,))
+            wqkv = m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d))
+            bqkv = m.wspan(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,))
             m._lin(y, wqkv, bqkv, self.qkv)
             cache = self.self_kv[i]
             F.kv_append(self.qkv[:, d:], 3 * d, cache, 2 * d, sb, B, 2 * d, t_dev, T_max)
@@ -251,6 +251,19 @@ class _Decoder:
         return gen[:, :L]
 
 
+def total_length(cfg, gc, P, max_length=None, max_new_tokens=None):
+    """Length cap of prompt + generated tokens, HF _set_max_new_tokens_and_length
+    (generation_whisper.py:1919-1945): max_new_tokens counts after the P prompt tokens; a max_length
+    (the call's, else generation_config's) is raised by the min(max_target_positions // 2 - 1, P)
+    initial tokens; both capped at max_target_positions."""
+    if max_new_tokens is not None:
+        total = P + int(max_new_tokens)
+    else:
+        ml = max_length or gc.max_length or cfg.max_target_positions
+        total = int(ml) + min(cfg.max_target_positions // 2 - 1, P)
+    return min(total, cfg.max_target_positions)
+
+
 def retrieve_segment(seq, seek_num_frames, ts_begin=50364, input_stride=2):
     """HF `_retrieve_segment` (generation_whisper.py), token part: split a window's tokens at
     consecutive timestamp pairs -> (segments, seek offset in feature frames)."""
@@ -303,7 +316,7 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     if encoder_outputs is not None:
         enc = encoder_outputs.last_hidden_state if hasattr(encoder_outputs, "last_hidden_state") else encoder_outputs[0]
         B, Tk = enc.shape[0], enc.shape[1]
-        enc16 = enc.reshape(-1, cfg.d_model).to(model.device, torch.bfloat16).contiguous()
+        enc16 = enc.reshape(-1, cfg.d_model).to(model.device, model.act_dtype).contiguous()
     else:
         conv_in = model.conv_input(input_features)
         enc16 = model.encode(conv_in)
@@ -316,11 +329,7 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     else:
         prompt = torch.tensor(build_prompt(gc, language, task, return_timestamps), dtype=torch.int64)[None].repeat(B, 1)
     P = prompt.shape[1]
-    if max_new_tokens is not None:
-        max_length = P + int(max_new_tokens)
-    if max_length is None:
-        max_length = gc.max_length or cfg.max_target_positions
-    max_length = min(int(max_length), cfg.max_target_positions)
+    max_length = total_length(cfg, gc, P, max_length, max_new_tokens)
     if P >= max_length:
         return torch.empty(B, 0, dtype=torch.int64, device=model.device)
     dec = _Decoder(model, gc, B, Tk, P, max_length, bool(return_timestamps), use_graph)
@@ -409,11 +418,7 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                     prev.extend(st[:-1] if len(st) > 2 and st[-2] >= ts_begin else st)
                 prompt = [int(prev_sot)] + prev[-cut_off:] + init
             P = len(prompt)
-            if max_new_tokens is not None:
-                ml = P + int(max_new_tokens)
-            else:
-                ml = int(max_length or gc.max_length or cfg.max_target_positions)
-            ml = min(ml, cfg.max_target_positions)
+            ml = total_length(cfg, gc, P, max_length, max_new_tokens)
             if P >= ml:
                 raise ValueError(f"prompt of {P} tokens leaves no room below max_length {ml}")
             dec = decoder(P, ml)

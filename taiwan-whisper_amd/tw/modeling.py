@@ -43,8 +43,9 @@ def padded_vocab(V: int) -> int:
 
 
 def fp32_compute_supported() -> bool:
-    """True once the fp32-arithmetic path (mixed_precision="no") is built into libtw_hip.so."""
-    return False
+    """The fp32-arithmetic path (mixed_precision="no": tw_gemm_f32 / tw_attn_*_f32 and the fp32 variants of
+    the loss, decode and selection kernels) is part of libtw_hip.so."""
+    return True
 
 # ---------------------------------------------------------------------------------------------
 # parameter layout
@@ -199,11 +200,16 @@ class _Group:
 class WhisperForConditionalGeneration:
     main_input_name = "input_features"
 
-    def __init__(self, config: WhisperConfig, dtype=torch.float32, device="cuda"):
+    def __init__(self, config: WhisperConfig, dtype=torch.float32, device="cuda", compute: str = "bf16"):
+        """dtype: parameter storage (fp32 master + bf16 mirror, or bf16 only).  compute: "bf16" = CUDA bf16
+        autocast's rounding points (mixed_precision="bf16", every reference launcher); "fp32" = plain fp32
+        arithmetic end to end (mixed_precision="no", the reference's default --dtype float32; needs the
+        fp32 master)."""
         if isinstance(config, dict):
             config = WhisperConfig(**config)
         self.config = config
         self.dtype = dtype
+        self.compute = "bf16"
         self.device = torch.device(device)
         self.Vp = padded_vocab(config.vocab_size)
         self.segs = engine_segments(config)
@@ -218,6 +224,25 @@ class WhisperForConditionalGeneration:
         self.model.encoder = _Group(self, "model.encoder")
         self.model.decoder = _Group(self, "model.decoder")
         self.proj_out = _Group(self, "model.decoder.embed_tokens")
+        self.set_compute(compute)
+
+    def set_compute(self, compute: str):
+        if compute not in ("bf16", "fp32"):
+            raise ValueError(f"compute must be 'bf16' or 'fp32', got {compute!r}")
+        if compute == "fp32" and self.dtype != torch.float32:
+            raise ValueError("fp32 arithmetic needs fp32 parameters (torch_dtype=torch.float32)")
+        self.compute = compute
+        return self
+
+    @property
+    def act_dtype(self):
+        """dtype of every GEMM / attention operand and output: bf16 under autocast, fp32 on the fp32 path."""
+        return torch.float32 if self.compute == "fp32" else torch.bfloat16
+
+    def act_grad(self, g: torch.Tensor) -> torch.Tensor:
+        """gradient entering a GEMM: rounded to bf16 under autocast (the grad of a bf16 activation),
+        unchanged on the fp32 path."""
+        return g if self.compute == "fp32" else _bf16(g)
 
     # ------------------------------------------------------------------ state dict / IO
     @property
@@ -280,20 +305,20 @@ class WhisperForConditionalGeneration:
         return self.store.v32(n) if self.store.p32 is not None else self._ln32[n]
 
     @classmethod
-    def from_state_dict(cls, config, sd, dtype=torch.float32, device="cuda"):
-        m = cls(config, dtype=dtype, device=device)
+    def from_state_dict(cls, config, sd, dtype=torch.float32, device="cuda", compute="bf16"):
+        m = cls(config, dtype=dtype, device=device, compute=compute)
         m.load_state_dict(sd, strict=False)
         return m
 
     @classmethod
     def from_pretrained(cls, path, torch_dtype=None, attn_implementation=None, low_cpu_mem_usage=True, config=None,
-                        device="cuda", **kw):
+                        device="cuda", compute="bf16", **kw):
         from safetensors.torch import load_file
         cfg = config if config is not None else WhisperConfig.from_pretrained(path)
         if isinstance(cfg, dict):
             cfg = WhisperConfig(**cfg)
         sd = load_file(os.path.join(path, "model.safetensors"))
-        m = cls.from_state_dict(cfg, sd, dtype=torch_dtype or torch.float32, device=device)
+        m = cls.from_state_dict(cfg, sd, dtype=torch_dtype or torch.float32, device=device, compute=compute)
         gp = os.path.join(path, "generation_config.json")
         if os.path.exists(gp):
             with open(gp) as f:
@@ -382,7 +407,14 @@ class WhisperForConditionalGeneration:
 
     # ------------------------------------------------------------------ building blocks
     def _w16(self, n):
-        return self.store.v16(n)
+        """weight as the GEMMs read it: the bf16 mirror (autocast's weight cast), or the fp32 master on
+        the fp32 path."""
+        return self.store.v32(n) if self.compute == "fp32" else self.store.v16(n)
+
+    def wspan(self, first, last, shape):
+        """fused projection weight / bias spanning adjacent segments (compute dtype)."""
+        buf = self.store.p32 if self.compute == "fp32" else self.store.p16
+        return self.store.span(buf, first, last, shape)
 
     def _lin(self, x, w, b, out, flags=F.GEMM_ROUND, res=None, aux=None, M=None):
         M = x.shape[0] if M is None else M
@@ -392,8 +424,8 @@ class WhisperForConditionalGeneration:
                flags=flags)
         return out
 
-    def _ln(self, x, name, out_dtype=torch.bfloat16, save=None):
-        y = torch.empty(x.shape, dtype=out_dtype, device=self.device)
+    def _ln(self, x, name, out_dtype=None, save=None):
+        y = torch.empty(x.shape, dtype=out_dtype or self.act_dtype, device=self.device)
         mean = rstd = None
         if save is not None:
             mean = torch.empty(x.shape[0], dtype=torch.float32, device=self.device)
@@ -409,11 +441,11 @@ class WhisperForConditionalGeneration:
         sv = {} if tape is not None else None
         y = self._ln(x, p + "_layer_norm", save=sv)
         M = B * T
-        qkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=self.device)
-        wqkv = self.store.span(self.store.p16, p + ".q_proj.weight", p + ".v_proj.weight", (3 * d, d))
-        bqkv = self.store.span(self.store.p16, p + ".q_proj.bias", p + ".v_proj.bias", (3 * d,))
+        qkv = torch.empty(M, 3 * d, dtype=self.act_dtype, device=self.device)
+        wqkv = self.wspan(p + ".q_proj.weight", p + ".v_proj.weight", (3 * d, d))
+        bqkv = self.wspan(p + ".q_proj.bias", p + ".v_proj.bias", (3 * d,))
         self._lin(y, wqkv, bqkv, qkv)
-        o = torch.empty(M, d, dtype=torch.bfloat16, device=self.device)
+        o = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         lse = torch.empty(B * H * T, dtype=torch.float32, device=self.device) if tape is not None else None
         F.attn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, o, d, lse, B, H, T, T, causal, 0.125)
         out = torch.empty(M, d, dtype=self.stream_dtype, device=self.device) if tape is not None else x
@@ -429,14 +461,14 @@ class WhisperForConditionalGeneration:
         sv = {} if tape is not None else None
         y = self._ln(x, p + "_layer_norm", save=sv)
         M = B * T
-        q = torch.empty(M, d, dtype=torch.bfloat16, device=self.device)
+        q = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         self._lin(y, self._w16(p + ".q_proj.weight"), self._w16(p + ".q_proj.bias"), q)
         if kv is None:
-            kv = torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=self.device)
-            wkv = self.store.span(self.store.p16, p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
-            bkv = self.store.span(self.store.p16, p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
+            kv = torch.empty(B * Tk, 2 * d, dtype=self.act_dtype, device=self.device)
+            wkv = self.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
+            bkv = self.wspan(p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
             self._lin(enc16, wkv, bkv, kv)
-        o = torch.empty(M, d, dtype=torch.bfloat16, device=self.device)
+        o = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         lse = torch.empty(B * H * T, dtype=torch.float32, device=self.device) if tape is not None else None
         F.attn_fwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, o, d, lse, B, H, T, Tk, False, 0.125)
         out = torch.empty(M, d, dtype=self.stream_dtype, device=self.device) if tape is not None else x
@@ -450,8 +482,8 @@ class WhisperForConditionalGeneration:
         sv = {} if tape is not None else None
         y = self._ln(x, p + ".final_layer_norm", save=sv)
         f = self.store.segs[p + ".fc1.weight"][0]
-        h = torch.empty(M, f, dtype=torch.bfloat16, device=self.device)
-        pre = torch.empty(M, f, dtype=torch.bfloat16, device=self.device) if tape is not None else None
+        h = torch.empty(M, f, dtype=self.act_dtype, device=self.device)
+        pre = torch.empty(M, f, dtype=self.act_dtype, device=self.device) if tape is not None else None
         self._lin(y, self._w16(p + ".fc1.weight"), self._w16(p + ".fc1.bias"), h, aux=pre,
                   flags=F.GEMM_ROUND | F.GEMM_GELU | (F.GEMM_AUX_OUT if tape is not None else 0))
         out = torch.empty(M, self.config.d_model, dtype=self.stream_dtype, device=self.device) \
@@ -463,29 +495,31 @@ class WhisperForConditionalGeneration:
 
     # ------------------------------------------------------------------ encoder / decoder
     def conv_input(self, input_features: torch.Tensor) -> torch.Tensor:
-        """[B, 80, 3000] fp32 -> time-major padded bf16 [B, 3002, 80] (the log-mel kernel emits
-        this directly; this path serves callers that hand over input_features)."""
+        """[B, 80, 3000] fp32 -> time-major padded [B, 3002, 80] in the compute dtype (the log-mel kernel
+        emits the bf16 one directly; this path serves callers that hand over input_features)."""
         B, nm, T = input_features.shape
         if T != 2 * self.config.max_source_positions:
             raise ValueError(f"Whisper expects the mel input features to be of length "
                              f"{2 * self.config.max_source_positions}, but found {T}.")
-        xt = torch.empty(B, T + 2, nm, dtype=torch.bfloat16, device=self.device)
+        xt = torch.empty(B, T + 2, nm, dtype=self.act_dtype, device=self.device)
         F.mel_to_conv_input(input_features.to(self.device, torch.float32).contiguous(), xt)
         return xt
 
     def encode(self, conv_in: torch.Tensor, tape=None) -> torch.Tensor:
-        """conv_in [B, 3002, 80] bf16 -> encoder_last_hidden_state [B*1500, d] bf16."""
+        """conv_in [B, 3002, 80] -> encoder_last_hidden_state [B*1500, d] (compute dtype)."""
         cfg, d = self.config, self.config.d_model
         B, T2 = conv_in.shape[0], conv_in.shape[1] - 2
         T = T2 // 2
         nm = cfg.num_mel_bins
-        H1 = torch.empty(B, T2 + 2, d, dtype=torch.bfloat16, device=self.device)
+        if conv_in.dtype != self.act_dtype:
+            raise ValueError(f"conv input is {conv_in.dtype}, this model computes in {self.act_dtype}")
+        H1 = torch.empty(B, T2 + 2, d, dtype=self.act_dtype, device=self.device)
         H1[:, 0].zero_()
         H1[:, T2 + 1].zero_()
         pre1 = pre2 = None
         if tape is not None:
-            pre1 = torch.empty(B, T2, d, dtype=torch.bfloat16, device=self.device)
-            pre2 = torch.empty(B, T, d, dtype=torch.bfloat16, device=self.device)
+            pre1 = torch.empty(B, T2, d, dtype=self.act_dtype, device=self.device)
+            pre2 = torch.empty(B, T, d, dtype=self.act_dtype, device=self.device)
         gf = F.GEMM_ROUND | F.GEMM_GELU | (F.GEMM_AUX_OUT if tape is not None else 0)
         F.gemm(conv_in, self._w16("model.encoder.conv1.weight"), H1[:, 1:], T2, d, 3 * nm, lda=nm, ldb=3 * nm,
                ldc=d, batch=B, sA=(T2 + 2) * nm, sC=(T2 + 2) * d, bias=self._w16("model.encoder.conv1.bias"),
@@ -522,7 +556,7 @@ class WhisperForConditionalGeneration:
         return x
 
     def decode(self, ids: torch.Tensor, enc16: torch.Tensor, Tk: int, tape=None) -> torch.Tensor:
-        """ids [B, T] int64 (device), enc16 [B*Tk, d] bf16 -> final decoder hidden [B*T, d] bf16."""
+        """ids [B, T] int64 (device), enc16 [B*Tk, d] -> final decoder hidden [B*T, d] (compute dtype)."""
         cfg = self.config
         B, T = ids.shape
         if T > cfg.max_target_positions:
@@ -542,10 +576,10 @@ class WhisperForConditionalGeneration:
         return h
 
     def lm_head(self, h16: torch.Tensor, out=None) -> torch.Tensor:
-        """tied proj_out: [M, d] bf16 -> bf16 logits [M, Vp] (pad columns are 0)."""
+        """tied proj_out: [M, d] -> logits [M, Vp] in the compute dtype (pad columns are 0)."""
         M = h16.shape[0]
         if out is None:
-            out = torch.empty(M, self.Vp, dtype=torch.bfloat16, device=self.device)
+            out = torch.empty(M, self.Vp, dtype=self.act_dtype, device=self.device)
         E = self._w16("model.decoder.embed_tokens.weight")
         F.gemm(h16, E, out, M, self.Vp, self.config.d_model, lda=h16.stride(0), ldb=self.config.d_model,
                ldc=self.Vp, flags=F.GEMM_ROUND, algo_N=self.config.vocab_size)
@@ -559,7 +593,7 @@ class WhisperForConditionalGeneration:
             enc = encoder_outputs.last_hidden_state if hasattr(encoder_outputs, "last_hidden_state") \
                 else encoder_outputs[0]
             B = enc.shape[0]
-            enc16 = enc.reshape(-1, cfg.d_model).to(self.device, torch.bfloat16).contiguous()
+            enc16 = enc.reshape(-1, cfg.d_model).to(self.device, self.act_dtype).contiguous()
             Tk = enc.shape[1]
         else:
             if conv_input is None:
@@ -642,7 +676,8 @@ class Backward:
         if out is None:
             return
         lo, hi = cols_slice
-        F.colsum(g[:, lo:] if lo else g, g.stride(0), g.shape[0], hi - lo, out, accum=True, round_bf16=True)
+        F.colsum(g[:, lo:] if lo else g, g.stride(0), g.shape[0], hi - lo, out, accum=True,
+                 round_bf16=self.m.compute != "fp32")
 
     def ln(self, sv, name, dy, dx):
         x, mean, rstd, _ = sv[name]
@@ -663,16 +698,16 @@ class Backward:
     # ------------------------------------------------------------------
     def mlp(self, p, st, dx):
         m = self.m
-        g = _bf16(dx)
+        g = m.act_grad(dx)
         M = g.shape[0]
         self.dW(g, st["h"], m.gv(p + ".fc2.weight"), M)
         self.db(g, (0, g.shape[1]), m.gv(p + ".fc2.bias"))
         f = st["h"].shape[1]
-        dpre = torch.empty(M, f, dtype=torch.bfloat16, device=self.dev)
+        dpre = torch.empty(M, f, dtype=m.act_dtype, device=self.dev)
         self.dX(g, m._w16(p + ".fc2.weight"), dpre, flags=F.GEMM_ROUND | F.GEMM_DGELU, aux=st["pre"])
         self.dW(dpre, st["y"], m.gv(p + ".fc1.weight"), M)
         self.db(dpre, (0, f), m.gv(p + ".fc1.bias"))
-        dy = torch.empty(M, m.config.d_model, dtype=torch.bfloat16, device=self.dev)
+        dy = torch.empty(M, m.config.d_model, dtype=m.act_dtype, device=self.dev)
         self.dX(dpre, m._w16(p + ".fc1.weight"), dy)
         self.ln(st["sv"], p + ".final_layer_norm", dy, dx)
 
@@ -682,20 +717,20 @@ class Backward:
         H = d // 64
         B, T = st["B"], st["T"]
         M = B * T
-        g = _bf16(dx)
+        g = m.act_grad(dx)
         self.dW(g, st["o"], m.gv(p + ".out_proj.weight"), M)
         self.db(g, (0, d), m.gv(p + ".out_proj.bias"))
-        do = torch.empty(M, d, dtype=torch.bfloat16, device=self.dev)
+        do = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
         self.dX(g, m._w16(p + ".out_proj.weight"), do)
         qkv = st["qkv"]
-        dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=self.dev)
+        dqkv = torch.empty(M, 3 * d, dtype=m.act_dtype, device=self.dev)
         F.attn_bwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, st["o"], d, do, d, st["lse"], dqkv, 3 * d,
                    dqkv[:, d:], 3 * d, dqkv[:, 2 * d:], 3 * d, B, H, T, T, st["causal"], 0.125)
         self.dW(dqkv, st["y"], self.span_grad(p + ".q_proj.weight", p + ".v_proj.weight", (3 * d, d)), M)
         self.db(dqkv, (0, d), m.gv(p + ".q_proj.bias"))
         self.db(dqkv, (2 * d, 3 * d), m.gv(p + ".v_proj.bias"))
-        dy = torch.empty(M, d, dtype=torch.bfloat16, device=self.dev)
-        wqkv = m.store.span(m.store.p16, p + ".q_proj.weight", p + ".v_proj.weight", (3 * d, d))
+        dy = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
+        wqkv = m.wspan(p + ".q_proj.weight", p + ".v_proj.weight", (3 * d, d))
         self.dX(dqkv, wqkv, dy)
         self.ln(st["sv"], p + "_layer_norm", dy, dx)
 
@@ -705,25 +740,25 @@ class Backward:
         H = d // 64
         B, T, Tk = st["B"], st["T"], st["Tk"]
         M = B * T
-        g = _bf16(dx)
+        g = m.act_grad(dx)
         self.dW(g, st["o"], m.gv(p + ".out_proj.weight"), M)
         self.db(g, (0, d), m.gv(p + ".out_proj.bias"))
-        do = torch.empty(M, d, dtype=torch.bfloat16, device=self.dev)
+        do = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
         self.dX(g, m._w16(p + ".out_proj.weight"), do)
         kv = st["kv"]
-        dq = torch.empty(M, d, dtype=torch.bfloat16, device=self.dev)
-        dkv = torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=self.dev)
+        dq = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
+        dkv = torch.empty(B * Tk, 2 * d, dtype=m.act_dtype, device=self.dev)
         F.attn_bwd(st["q"], d, kv, 2 * d, kv[:, d:], 2 * d, st["o"], d, do, d, st["lse"], dq, d, dkv, 2 * d,
                    dkv[:, d:], 2 * d, B, H, T, Tk, False, 0.125)
         self.dW(dq, st["y"], m.gv(p + ".q_proj.weight"), M)
         self.db(dq, (0, d), m.gv(p + ".q_proj.bias"))
-        dy = torch.empty(M, d, dtype=torch.bfloat16, device=self.dev)
+        dy = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
         self.dX(dq, m._w16(p + ".q_proj.weight"), dy)
         self.ln(st["sv"], p + "_layer_norm", dy, dx)
         self.dW(dkv, enc16, self.span_grad(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d)), B * Tk)
         self.db(dkv, (d, 2 * d), m.gv(p + ".v_proj.bias"))
         if d_enc is not None:
-            wkv = m.store.span(m.store.p16, p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
+            wkv = m.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
             self.dX(dkv, wkv, d_enc, flags=F.GEMM_ROUND | F.GEMM_ACCUM)
 
     # ------------------------------------------------------------------
@@ -735,7 +770,7 @@ class Backward:
         E16 = m._w16("model.decoder.embed_tokens.weight")
         gE = m.gv("model.decoder.embed_tokens.weight")
         # LM head (tied): dh = bf16(dlogits E), dE += bf16(dlogits^T h)
-        dh = torch.empty(M, d, dtype=torch.bfloat16, device=self.dev)
+        dh = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
         F.gemm(dlogits, E16, dh, M, d, m.Vp, lda=m.Vp, ldb=d, ldc=d, b_trans=True, flags=F.GEMM_ROUND)
         if gE is not None:
             F.gemm(dlogits, h16, gE, m.Vp, d, M, lda=m.Vp, ldb=d, ldc=d, a_trans=True, b_trans=True,
@@ -783,9 +818,9 @@ class Backward:
         g1w, g2w = m.gv("model.encoder.conv1.weight"), m.gv("model.encoder.conv2.weight")
         if g1w is None and g2w is None:
             return
-        dpre2 = torch.empty(B * T, d, dtype=torch.bfloat16, device=self.dev)
+        dpre2 = torch.empty(B * T, d, dtype=m.act_dtype, device=self.dev)
         F.gelu_bwd(dx0, st["pre2"].view(B * T, d), dpre2)
-        A2 = torch.empty(B * T, 3 * d, dtype=torch.bfloat16, device=self.dev)
+        A2 = torch.empty(B * T, 3 * d, dtype=m.act_dtype, device=self.dev)
         F.im2col3(st["H1"], T2 + 2, A2, B, T, 2, d)
         self.dW(dpre2, A2, g2w, B * T)
         self.db(dpre2, (0, d), m.gv("model.encoder.conv2.bias"))
@@ -793,9 +828,9 @@ class Backward:
         self.dX(dpre2, m._w16("model.encoder.conv2.weight"), dA2, flags=0)
         dH1 = torch.empty(B * T2, d, dtype=torch.float32, device=self.dev)
         F.col2im_s2(dA2, dH1, B, T2, T, d)
-        dpre1 = torch.empty(B * T2, d, dtype=torch.bfloat16, device=self.dev)
+        dpre1 = torch.empty(B * T2, d, dtype=m.act_dtype, device=self.dev)
         F.gelu_bwd(dH1, st["pre1"].view(B * T2, d), dpre1)
-        A1 = torch.empty(B * T2, 3 * nm, dtype=torch.bfloat16, device=self.dev)
+        A1 = torch.empty(B * T2, 3 * nm, dtype=m.act_dtype, device=self.dev)
         F.im2col3(st["conv_in"], T2 + 2, A1, B, T2, 1, nm)
         self.dW(dpre1, A1, g1w, B * T2)
         self.db(dpre1, (0, d), m.gv("model.encoder.conv1.bias"))

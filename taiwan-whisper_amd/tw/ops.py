@@ -46,11 +46,20 @@ def _need(t: torch.Tensor, n_elems: int, what: str):
 
 
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, bias=None, res=None,
-         ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0, algo_N=None):
-    """C[b] = epi(alpha * A[b] @ B[b]^T); A bf16 [M][K] (a_trans: [K][M]); B bf16 [N][K] (b_trans: [K][N])."""
+         ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0, algo_N=None,
+         batch_inner=1, sA_in=0, sB_in=0, sC_in=0):
+    """C[b] = epi(alpha * A[b] @ B[b]^T); A [M][K] (a_trans: [K][M]); B [N][K] (b_trans: [K][N]).
+    bf16 operands -> tw_gemm_bf16 (autocast rounding points); fp32 operands -> tw_gemm_f32 (the fp32
+    path: every operand and epilogue tensor fp32, nothing rounded)."""
     if M <= 0 or N <= 0:
         return C
-    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "tw.gemm: A and B must be bf16"
+    if A.dtype == torch.float32 or B.dtype == torch.float32:
+        return gemm_f32(A, B, C, M, N, K, lda=lda, ldb=ldb, ldc=ldc, a_trans=a_trans, b_trans=b_trans, alpha=alpha,
+                        bias=bias, res=res, ldr=ldr, res_mod=res_mod, aux=aux, ldaux=ldaux, flags=flags, batch=batch,
+                        sA=sA, sB=sB, sC=sC, sR=sR, sAux=sAux, algo_N=algo_N, batch_inner=batch_inner, sA_in=sA_in,
+                        sB_in=sB_in, sC_in=sC_in)
+    assert batch_inner == 1, "tw.gemm: two-level batches are an fp32-path feature"
+    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "tw.gemm: A and B must be bf16 (or both fp32)"
     _need(A, (batch - 1) * sA + ((K - 1) * lda + M if a_trans else (M - 1) * lda + K), "gemm A")
     _need(B, (batch - 1) * sB + ((K - 1) * ldb + N if b_trans else (N - 1) * ldb + K), "gemm B")
     _need(C, (batch - 1) * sC + (M - 1) * ldc + N, "gemm C")
@@ -100,6 +109,8 @@ def layernorm_bwd(x, w, mean, rstd, dy, dx, dw, db, dx_accum=True, workspace=Non
 
 
 def attn_fwd(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale):
+    if q.dtype == torch.float32:
+        return attn_fwd_f32(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale)
     hd = 64
     for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o")):
         assert t.dtype == torch.bfloat16
@@ -113,6 +124,9 @@ def attn_fwd(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale):
 
 def attn_bwd(q, ldq, k, ldk, v, ldv, o, ldo, do, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Tq, Tk, causal,
              scale, workspace=None):
+    if q.dtype == torch.float32:
+        return attn_bwd_f32(q, ldq, k, ldk, v, ldv, o, ldo, do, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Tq, Tk,
+                            causal, scale)
     hd = 64
     for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o"),
                          (do, lddo, Tq, "do"), (dq, lddq, Tq, "dq"), (dk, lddk, Tk, "dk"), (dv, lddv, Tk, "dv")):
@@ -129,15 +143,16 @@ def attn_bwd(q, ldq, k, ldk, v, ldv, o, ldo, do, lddo, lse, dq, lddq, dk, lddk, 
 def kl_ce(s_logits, t_logits, labels, V, n_valid, T=2.0, ce_w=0.8, kl_w=1.0, grad_scale=1.0, dlogits=None,
           row_out=None, out3=None):
     rows, ld = s_logits.shape
-    assert t_logits.shape == s_logits.shape and s_logits.dtype == torch.bfloat16 and t_logits.dtype == torch.bfloat16
+    assert t_logits.shape == s_logits.shape and s_logits.dtype == t_logits.dtype
+    assert s_logits.dtype in (torch.bfloat16, torch.float32)
     assert labels.dtype == torch.int64 and labels.numel() == rows and n_valid.dtype == torch.int32
     if row_out is None:
         row_out = torch.empty(rows * 2, dtype=torch.float32, device=s_logits.device)
     if out3 is None:
         out3 = torch.empty(3, dtype=torch.float32, device=s_logits.device)
     if dlogits is not None:
-        assert dlogits.shape == s_logits.shape and dlogits.dtype == torch.bfloat16
-    call("tw_kl_ce", s_logits.data_ptr(), t_logits.data_ptr(), ld, labels.data_ptr(), rows, V, float(T),
+        assert dlogits.shape == s_logits.shape and dlogits.dtype == s_logits.dtype
+    call("tw_kl_ce", s_logits.data_ptr(), t_logits.data_ptr(), ld, _dt(s_logits), labels.data_ptr(), rows, V, float(T),
          float(ce_w), float(kl_w), n_valid.data_ptr(), float(grad_scale), row_out.data_ptr(), out3.data_ptr(),
          _ptr(dlogits), _stream())
     return out3, row_out
@@ -158,7 +173,11 @@ def logmel(wav, basis, mel_start, mel_w, mel_out, conv_in=None, workspace=None):
 
 def mel_to_conv_input(mel, xt):
     B, nmel, T = mel.shape
-    assert xt.shape == (B, T + 2, nmel) and xt.dtype == torch.bfloat16 and mel.is_contiguous()
+    assert xt.shape == (B, T + 2, nmel) and mel.is_contiguous() and mel.dtype == torch.float32
+    if xt.dtype == torch.float32:
+        call("tw_mel_to_conv_input_f32", mel.data_ptr(), xt.data_ptr(), B, nmel, T, _stream())
+        return xt
+    assert xt.dtype == torch.bfloat16
     call("tw_mel_to_conv_input", mel.data_ptr(), xt.data_ptr(), B, nmel, T, _stream())
     return xt
 
@@ -227,7 +246,9 @@ def adamw(p, g, m, v, p_bf16, lr, b1, b2, eps, wd, step, norm=None, max_norm=0.0
 def im2col3(src, src_rows, dst, B, T_out, stride, C):
     _need(src, (B - 1) * src_rows * C + ((T_out - 1) * stride + 3) * C, "im2col src")
     _need(dst, B * T_out * 3 * C, "im2col dst")
-    call("tw_im2col3", src.data_ptr(), src_rows, dst.data_ptr(), B, T_out, stride, C, _stream())
+    assert src.dtype == dst.dtype
+    fn = "tw_im2col3_f32" if src.dtype == torch.float32 else "tw_im2col3"
+    call(fn, src.data_ptr(), src_rows, dst.data_ptr(), B, T_out, stride, C, _stream())
 
 
 def col2im_s2(dA, dX, B, T_in, T_out, C):
@@ -250,7 +271,12 @@ def count_valid(labels, out):
 
 
 def gelu_bwd(g, pre, out):
-    assert pre.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and g.numel() == pre.numel() == out.numel()
+    assert g.numel() == pre.numel() == out.numel()
+    if pre.dtype == torch.float32:
+        assert g.dtype == torch.float32 and out.dtype == torch.float32
+        call("tw_gelu_bwd_f32", g.data_ptr(), pre.data_ptr(), out.data_ptr(), g.numel(), _stream())
+        return out
+    assert pre.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
     call("tw_gelu_bwd", g.data_ptr(), _dt(g), pre.data_ptr(), out.data_ptr(), g.numel(), _stream())
     return out
 
@@ -261,7 +287,7 @@ def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_de
     With tk_dev the host cannot know Tk: tk_max bounds the rows checked for extent."""
     hd = 64
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
-        assert t.dtype == torch.bfloat16, nm
+        assert t.dtype == q.dtype and t.dtype in (torch.bfloat16, torch.float32), nm
     rows = Tk if tk_dev is None else tk_max
     _need(q, (B - 1) * sqb + H * hd, "decode q")
     _need(k, (B - 1) * skb + (rows - 1) * ldk + H * hd, "decode k")
@@ -270,7 +296,7 @@ def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_de
     if tk_dev is not None:
         assert tk_dev.dtype == torch.int32 and tk_max is not None
     call("tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb, o.data_ptr(), sob,
-         B, H, Tk, _ptr(tk_dev), hd, float(scale), _stream())
+         B, H, Tk, _ptr(tk_dev), hd, float(scale), _dt(q), _stream())
     return o
 
 
@@ -287,30 +313,30 @@ def token_bitmask(ids, V, device):
 
 def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids,
                   t_dev=None, begin_col=-1):
-    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
-    assert done.dtype == torch.uint8
+    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8
     _need(logits, (B - 1) * ld + V, "greedy logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "greedy ids")
     _need(done, B, "greedy done"); _need(next_ids, B, "greedy next")
     for m, nm in ((suppress_bits, "suppress"), (begin_bits, "begin")):
         if m is not None:
             _need(m, (V + 31) // 32, f"greedy {nm} mask")
-    call("tw_greedy_select", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
+    call("tw_greedy_select", logits.data_ptr(), ld, _dt(logits), B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
          int(eos), done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev),
          int(begin_col), _stream())
 
 
 def greedy_select_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids, col, next_ids, last_ts,
                      begin_col, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
-    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
-    assert done.dtype == torch.uint8 and last_ts.dtype == torch.int32
+    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8 and last_ts.dtype == torch.int32
     _need(logits, (B - 1) * ld + V, "greedy logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "greedy ids")
     _need(done, B, "greedy done"); _need(next_ids, B, "greedy next"); _need(last_ts, B, "greedy last_ts")
     for m, nm in ((suppress_bits, "suppress"), (begin_bits, "begin")):
         if m is not None:
             _need(m, (V + 31) // 32, f"greedy {nm} mask")
-    call("tw_greedy_select_ts", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(eos),
+    call("tw_greedy_select_ts", logits.data_ptr(), ld, _dt(logits), B, V, _ptr(suppress_bits), _ptr(begin_bits), int(eos),
          done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev), int(begin_col),
          int(ts_begin), int(no_ts), int(max_initial if max_initial is not None else -1), last_ts.data_ptr(),
          _stream())
@@ -322,12 +348,12 @@ def select_sample(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos,
     + running log-prob of the chosen token (sum_logp: float32[B])."""
     assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
     _need(sum_logp, B, "select sum_logp")
-    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
-    assert done.dtype == torch.uint8
+    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8
     _need(logits, (B - 1) * ld + V, "select logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "select ids")
     _need(done, B, "select done"); _need(next_ids, B, "select next")
-    call("tw_select_sample", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
+    call("tw_select_sample", logits.data_ptr(), ld, _dt(logits), B, V, _ptr(suppress_bits), _ptr(begin_bits), int(apply_begin),
          int(eos), done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev),
          int(begin_col), ctl.data_ptr(), sum_logp.data_ptr(), _stream())
 
@@ -336,12 +362,12 @@ def select_sample_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids
                      ctl, sum_logp, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
     assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
     _need(sum_logp, B, "select sum_logp")
-    assert logits.dtype == torch.bfloat16 and ids.dtype == torch.int64 and next_ids.dtype == torch.int64
-    assert done.dtype == torch.uint8 and last_ts.dtype == torch.int32
+    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8 and last_ts.dtype == torch.int32
     _need(logits, (B - 1) * ld + V, "select logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "select ids")
     _need(done, B, "select done"); _need(next_ids, B, "select next"); _need(last_ts, B, "select last_ts")
-    call("tw_select_sample_ts", logits.data_ptr(), ld, B, V, _ptr(suppress_bits), _ptr(begin_bits), int(eos),
+    call("tw_select_sample_ts", logits.data_ptr(), ld, _dt(logits), B, V, _ptr(suppress_bits), _ptr(begin_bits), int(eos),
          done.data_ptr(), ids.data_ptr(), ids.stride(0), col, next_ids.data_ptr(), _ptr(t_dev), int(begin_col),
          int(ts_begin), int(no_ts), int(max_initial if max_initial is not None else -1), last_ts.data_ptr(),
          ctl.data_ptr(), sum_logp.data_ptr(), _stream())
@@ -349,9 +375,9 @@ def select_sample_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids
 
 def token_logprob(logits, ld, B, V, token, out):
     """out[b] = log_softmax(logits[b, :V])[token] (float32)."""
-    assert logits.dtype == torch.bfloat16 and out.dtype == torch.float32
+    assert logits.dtype in (torch.bfloat16, torch.float32) and out.dtype == torch.float32
     _need(logits, (B - 1) * ld + V, "token_logprob logits"); _need(out, B, "token_logprob out")
-    call("tw_token_logprob", logits.data_ptr(), ld, B, V, int(token), out.data_ptr(), _stream())
+    call("tw_token_logprob", logits.data_ptr(), ld, _dt(logits), B, V, int(token), out.data_ptr(), _stream())
     return out
 
 
@@ -381,12 +407,82 @@ def embed_step(ids, tok, pos, out, t_dev, max_pos):
 
 
 def kv_append(src, ld_src, cache, ld_row, sb, B, n, t_dev, max_rows):
-    assert src.dtype == torch.bfloat16 and cache.dtype == torch.bfloat16 and t_dev.dtype == torch.int32
+    assert src.dtype == cache.dtype and src.dtype in (torch.bfloat16, torch.float32) and t_dev.dtype == torch.int32
     _need(src, (B - 1) * ld_src + n, "kv_append src")
     _need(cache, (B - 1) * sb + (max_rows - 1) * ld_row + n, "kv_append cache")
-    call("tw_kv_append", src.data_ptr(), ld_src, cache.data_ptr(), ld_row, sb, B, n, t_dev.data_ptr(), _stream())
+    call("tw_kv_append", src.data_ptr(), ld_src, cache.data_ptr(), ld_row, sb, B, n, _dt(src), t_dev.data_ptr(),
+         _stream())
 
 
 def step_advance(t_dev, by=1):
     assert t_dev.dtype == torch.int32 and t_dev.is_cuda
     call("tw_step_advance", t_dev.data_ptr(), int(by), _stream())
+
+
+# ----------------------------------------------------------------------------- fp32 arithmetic path
+def gemm_f32(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, bias=None, res=None,
+             ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0, algo_N=None,
+             batch_inner=1, sA_in=0, sB_in=0, sC_in=0):
+    """tw_gemm_f32: every tensor fp32; batch entry bz = bo * batch_inner + bi at offsets bo*s? + bi*s?_in."""
+    if M <= 0 or N <= 0:
+        return C
+    for t, nm in ((A, "A"), (B, "B"), (C, "C"), (bias, "bias"), (res, "res"), (aux, "aux")):
+        assert t is None or t.dtype == torch.float32, f"tw.gemm_f32: {nm} must be fp32"
+    assert batch % batch_inner == 0
+    nb = batch // batch_inner
+    _need(A, (nb - 1) * sA + (batch_inner - 1) * sA_in + ((K - 1) * lda + M if a_trans else (M - 1) * lda + K),
+          "gemm_f32 A")
+    _need(B, (nb - 1) * sB + (batch_inner - 1) * sB_in + ((K - 1) * ldb + N if b_trans else (N - 1) * ldb + K),
+          "gemm_f32 B")
+    _need(C, (nb - 1) * sC + (batch_inner - 1) * sC_in + (M - 1) * ldc + N, "gemm_f32 C")
+    flags &= ~GEMM_ROUND
+    if bias is not None:
+        _need(bias, N, "gemm_f32 bias")
+        flags |= GEMM_BIAS
+    if res is not None:
+        rows = res_mod if res_mod > 0 else M
+        _need(res, (nb - 1) * sR + (rows - 1) * ldr + N, "gemm_f32 residual")
+        flags |= GEMM_RES
+    if aux is not None:
+        _need(aux, (nb - 1) * sAux + (M - 1) * ldaux + N, "gemm_f32 aux")
+    fam = "gemm32_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
+    flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
+    KernelTimer.wrap(fam, flops, lambda: call(
+        "tw_gemm_f32", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, M, N, K,
+        batch, sA, sB, sC, batch_inner, sA_in, sB_in, sC_in, float(alpha), _ptr(bias), _ptr(res), ldr, sR, res_mod,
+        _ptr(aux), ldaux, sAux, flags, _stream()))
+    return C
+
+
+def _attn_ws(Tq, Tk, bufs, device, B, H):
+    """score workspace: as many (b, h) pairs per pass as fit in 512 MiB (at least one)."""
+    per = Tq * ((Tk + 3) // 4 * 4) * bufs
+    n = max(per, min(B * H * per, (512 << 20) // 4))
+    return workspace(n, device, "attn_f32"), n
+
+
+def attn_fwd_f32(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale):
+    hd = 64
+    for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o")):
+        assert t.dtype == torch.float32, nm
+        _need(t, (B * T - 1) * ld + H * hd, f"attn_f32 {nm}")
+    if lse is not None:
+        _need(lse, B * H * Tq, "attn_f32 lse")
+    ws, n = _attn_ws(Tq, Tk, 1, q.device, B, H)
+    call("tw_attn_fwd_f32", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, _ptr(lse),
+         B, H, Tq, Tk, hd, int(causal), float(scale), ws.data_ptr(), n, _stream())
+    return o
+
+
+def attn_bwd_f32(q, ldq, k, ldk, v, ldv, o, ldo, do, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Tq, Tk, causal,
+                 scale):
+    hd = 64
+    for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o"),
+                         (do, lddo, Tq, "do"), (dq, lddq, Tq, "dq"), (dk, lddk, Tk, "dk"), (dv, lddv, Tk, "dv")):
+        assert t.dtype == torch.float32, nm
+        _need(t, (B * T - 1) * ld + H * hd, f"attn_bwd_f32 {nm}")
+    _need(lse, B * H * Tq, "attn_bwd_f32 lse")
+    ws, n = _attn_ws(Tq, Tk, 2, q.device, B, H)
+    call("tw_attn_bwd_f32", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, do.data_ptr(),
+         lddo, lse.data_ptr(), dq.data_ptr(), lddq, dk.data_ptr(), lddk, dv.data_ptr(), lddv, B, H, Tq, Tk, hd,
+         int(causal), float(scale), ws.data_ptr(), n, _stream())

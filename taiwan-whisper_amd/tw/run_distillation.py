@@ -202,9 +202,11 @@ def load_models(args, device, tokenizer=None):
     creation (create_student_model.py:124-125)."""
     from .modeling import WhisperForConditionalGeneration
     from .student import mix_language_embeddings
+    compute = "fp32" if args.dtype == "float32" else "bf16"      # mixed_precision "no" / "bf16" (:815-823)
     teacher = WhisperForConditionalGeneration.from_pretrained(args.teacher_model_name_or_path,
-                                                              torch_dtype=teacher_dtype(args.dtype), device=device)
-    student = WhisperForConditionalGeneration.from_pretrained(args.model_name_or_path, device=device)
+                                                              torch_dtype=teacher_dtype(args.dtype), device=device,
+                                                              compute=compute)
+    student = WhisperForConditionalGeneration.from_pretrained(args.model_name_or_path, device=device, compute=compute)
     if args.mix_lang_emb:
         mix_language_embeddings(teacher, tokenizer if hasattr(tokenizer, "convert_tokens_to_ids") else None,
                                 languages=["zh", "en"])

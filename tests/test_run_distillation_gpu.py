@@ -146,3 +146,24 @@ def test_partial_accumulation_steps_at_end_of_dataloader():
     tr.train_step(batches[2], end_of_dataloader=True)
     assert tr.step == 2 and tr.micro == 0
     assert not torch.equal(before, s.store.p32)
+
+
+def test_entry_point_float32_dtype(tmp_path):
+    """--dtype float32 (the reference's default: mixed_precision="no", teacher in fp32,
+    run_distillation.py:815-823) trains and evaluates on the fp32 arithmetic path; --dtype float16
+    raises instead of silently running another precision."""
+    from tw.run_distillation import main
+    teacher, student = _model_dirs(str(tmp_path))
+    man = _corpus(str(tmp_path / "corpus"))
+    out = str(tmp_path / "out32")
+    common = ["--model_name_or_path", student, "--teacher_model_name_or_path", teacher, "--output_dir", out,
+              "--train_dataset_manifest", man, "--eval_dataset_manifest", man, "--per_device_train_batch_size", "2",
+              "--per_device_eval_batch_size", "3", "--learning_rate", "1e-4", "--save_steps", "100",
+              "--logging_steps", "1", "--freeze_encoder", "True", "--language", "zh", "--do_eval", "True",
+              "--predict_with_generate", "True", "--max_label_length", "64", "--byte_level_text_tokenizer", "True",
+              "--dataloader_num_workers", "2", "--streaming", "False", "--max_steps", "2", "--eval_steps", "2"]
+    res = main(common + ["--dtype", "float32"])
+    assert [h["step"] for h in res["train"]] == [1, 2]
+    assert all(np.isfinite(h["loss"]) for h in res["train"]) and np.isfinite(res["eval"][0]["loss"])
+    with pytest.raises(NotImplementedError):
+        main(common + ["--dtype", "float16", "--output_dir", str(tmp_path / "out16")])
