@@ -10,9 +10,9 @@ End to end, against HF Transformers run in fp32 (the fixtures of tests/golden/ma
     long-form with conditioning / thresholds (fallback.npz): token ids IDENTICAL to HF generate --
     north star "token ids bit-exact for greedy decode", no near-tie allowance;
   * the per-window average log-probs / no-speech probabilities of that long-form run: 1e-4;
-  * the distillation step on the micro config (micro_step.npz) and at c1 dims (cfg_c1.npz f32|...):
-    loss / CE / KL 2e-5 relative, per-tensor gradient norms 1e-3 relative, encoder output and logits
-    1e-4 relative L2.
+  * the distillation step on the micro config (micro_step.npz) and at c1 / c2 / c3 dims (cfg_c*.npz
+    f32|...): loss / CE / KL 2e-5 relative, per-tensor gradient norms 1e-3 relative, the sampled gradient
+    block and the encoder output 1e-4 relative L2.
 """
 import numpy as np
 import pytest
@@ -40,8 +40,8 @@ def rel(a, b):
 @pytest.mark.parametrize("M,N,K", [(200, 136, 72), (131, 257, 447), (1500, 64, 1500), (3, 384, 128)])
 def test_gemm_f32_layouts(a_t, b_t, M, N, K):
     from tw import ops
-    if (a_t and M % 4) or (b_t and N % 4) or (not a_t and K % 4 and False):
-        pytest.skip("n/a")
+    if (a_t and M % 4) or (b_t and N % 4):
+        pytest.skip("MN-major operands: lda / ldb = M / N must be a multiple of 4")
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
     A, Bm = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
     ref = A.double() @ Bm.double().T
@@ -253,6 +253,46 @@ def test_fp32_train_step_matches_hf_fp32_c1():
     c = mg.CFG_CASES["c1"]
     s, t, m, grad, batch = _step_f32(scfg, ws, tcfg, wt, feats, dec, lab, c["freeze_encoder"],
                                      c["freeze_embed_positions"])
+    for k, fk in (("loss", "loss"), ("ce_loss", "ce"), ("kl_loss", "kl")):
+        ref = float(g["f32|" + fk])
+        assert abs(m[k] - ref) / abs(ref) < 2e-5, (k, m[k], ref)
+    names = [str(n) for n in g["grad_names"]]
+    r = np.abs(_grad_norms(s, grad, names) - g["f32|grad_norms"]) / g["f32|grad_norms"]
+    assert r.max() < 1e-3, (names[int(r.argmax())], r.max())
+    p0 = "model.decoder.layers.0.fc1.weight"
+    o = s.store.offset[p0]
+    gsub = grad[o: o + s.store.numel(p0)].view(s.store.segs[p0])[::37, ::29]
+    assert rel(gsub, torch.from_numpy(g["f32|grad_dec0_fc1_sub"])) < 1e-4
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_fp32_train_step_matches_hf_fp32_large(name):
+    """c2 (small <- large-v2, full teacher forward, the whole student trained incl. conv stem) and c3
+    (distil-32-2 made by tw.student from the large-v2 teacher, shared frozen encoder, prompt quirk) at B=1
+    on the fp32 path vs HF fp32."""
+    import os, sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as mg
+    from oracle.weights import CONFIGS, make_weights
+    from tw.config import WhisperConfig
+    from tw.modeling import WhisperForConditionalGeneration
+    from tw.student import student_from_teacher
+    g = load_golden("cfg_" + name)
+    c = mg.CFG_CASES[name]
+    tcfg = CONFIGS[c["teacher"]]
+    wt = make_weights(tcfg, c["t_seed"], per_tensor=True, embed_std=mg.EMBED_STD)
+    feats, dec, lab = mg.cfg_case_batch(name)
+    student, scfg, ws = None, None, None
+    if c["student"] is None:
+        t32 = WhisperForConditionalGeneration.from_state_dict(WhisperConfig(**tcfg), {k: torch.from_numpy(v) for k, v in
+                                                                                      wt.items()}, dtype=torch.float32)
+        student = student_from_teacher(t32, decoder_layers=2)[0].set_compute("fp32")
+        del t32
+    else:
+        scfg = CONFIGS[c["student"]]
+        ws = make_weights(scfg, c["s_seed"], per_tensor=True, embed_std=mg.EMBED_STD)
+    s, t, m, grad, batch = _step_f32(scfg, ws, tcfg, wt, feats, dec, lab, c["freeze_encoder"],
+                                     c["freeze_embed_positions"], student=student)
     for k, fk in (("loss", "loss"), ("ce_loss", "ce"), ("kl_loss", "kl")):
         ref = float(g["f32|" + fk])
         assert abs(m[k] - ref) / abs(ref) < 2e-5, (k, m[k], ref)
