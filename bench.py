@@ -6,7 +6,13 @@ Workload (default, BASELINE config 3): 2-decoder-layer distil-whisper student ma
 create_student_model layer map from a large-v2 teacher, frozen shared encoder, batch 64 clips per
 GPU, bf16 autocast semantics, full step = GPU log-mel + student fwd + teacher fwd + fused KL/CE +
 student bwd + (DP all-reduce) + clip + AdamW.  `--config c2` runs config 2 (whisper-small student,
-trainable encoder, full large-v2 teacher forward, B = 32).  Random-init weights of the real
+trainable encoder, full large-v2 teacher forward, B = 32).  `--config c4` is the pseudo-labelling
+path (initial_inference.py / run_pseudo_labelling.py:917-922): large-v2 batched greedy transcription of
+512 synthetic 30 s clips (GPU log-mel + encoder + KV-cache decode, 224 new tokens per clip: eos is
+suppressed so the work is fixed), a step = one batch of --batch clips.  `--config c5` is
+the long-form eval path (run_eval.py:659-685): one 30-minute synthetic recording, long-form log-mel,
+sequential 30 s windows with timestamp tokens, cross-attention K/V projected once per window and reused
+by every step (a step = the whole recording; value = audio seconds per wall second).  Random-init weights of the real
 architectures (no checkpoints offline) and synthetic 30 s / 16 kHz sine clips + synthetic labels
 (SURVEY.md §8(d)); inputs are resident in HBM before the timed region.
 
@@ -138,18 +144,144 @@ def load_pmc(kernel_family):
     return d.get(kernel_family, {}).get("hbm_bytes_per_launch")
 
 
+def decode_bytes_per_step(cfg, B, t_avg, Tk=1500, elem=2):
+    """Algorithmic HBM bytes of one greedy decode step over B rows: every decoder weight once (the
+    per-layer Linears + LayerNorms, the tied head over the padded vocabulary), the cross-attention
+    K/V of every clip and layer, and the self-attention K/V rows 0..t (t_avg = mean step index)."""
+    d, f, L, Vp = cfg.d_model, cfg.decoder_ffn_dim, cfg.decoder_layers, (cfg.vocab_size + 63) // 64 * 64
+    weights = L * (6 * d * d + 2 * d * f) * elem + Vp * d * elem
+    cross = L * B * Tk * 2 * d * elem
+    self_kv = L * B * t_avg * 2 * d * elem
+    return weights + cross + self_kv
+
+
+def run_decode(args, device, rank, world, pg):
+    """c4 (batched greedy pseudo-labelling) and c5 (long-form eval) on large-v2 (random-init bf16:
+    the reference runs these in the checkpoint's dtype under its fp16/bf16 flag)."""
+    from tw.config import LARGE_V2_SUPPRESS, MODEL_DIMS, GenerationConfig, WhisperConfig
+    from tw.data import synthetic_audio
+    from tw.feature_extraction import WhisperFeatureExtractor
+    from tw.modeling import WhisperForConditionalGeneration, random_init_
+    from tw.profiling import KernelTimer
+    cfg = WhisperConfig(**MODEL_DIMS["large-v2"])
+    m = random_init_(WhisperForConditionalGeneration(cfg, dtype=torch.bfloat16, device=device), seed=0)
+    fe = WhisperFeatureExtractor(device=device)
+    c4 = args.config == "c4"
+    # c4: eos suppressed -> every clip decodes exactly --new-tokens (SURVEY.md §8d fixed work)
+    m.generation_config = GenerationConfig(suppress_tokens=LARGE_V2_SUPPRESS + ([50257] if c4 else []),
+                                           begin_suppress_tokens=[220, 50257], lang_to_id={"<|zh|>": 50260})
+    kw = dict(language="zh", task="transcribe", max_new_tokens=args.new_tokens)
+    if c4:
+        wavs = [synthetic_audio(args.batch, seed=1000 * rank + i, device=device) for i in range(2)]
+
+        def step(i):
+            mel, _ = fe.extract(wavs[i % 2], want_conv_input=False)
+            return m.generate(mel, **kw)
+        units_per_step, unit = args.batch, "utt/s"
+    else:
+        n = int(args.seconds * 16000)
+        wav = synthetic_audio(1, seed=1000 * rank, seconds=args.seconds, device=device, length=None)
+        mel_long, _ = fe.extract(wav, want_conv_input=False)           # features prepared outside the timed
+        mask = torch.ones(1, n // 160, dtype=torch.int32, device=device)   # region, as run_eval.py:567-589
+        trace = []
+
+        def step(i):
+            trace.clear()
+            return m.generate(mel_long, attention_mask=mask, return_timestamps=True, _trace=trace, **kw)
+        units_per_step, unit = args.seconds, "audio s/s"
+    for i in range(args.warmup):
+        if c4:
+            step(i)
+        else:      # warm-up on a 65 s prefix (the kernels and graph capture; not the full recording)
+            m.generate(mel_long[:, :, :6500], attention_mask=mask[:, :6500], return_timestamps=True, **kw)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = step(i)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if pg is not None:
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    if c4:
+        dec_steps = args.steps * (out.shape[1] + 3)                 # prompt prefill (3) + generated columns
+        B, t_avg = args.batch, 4 + out.shape[1] / 2
+    else:
+        dec_steps = args.steps * sum(len(t["raw"]) + len(t["prompt"]) - 1 for t in trace)
+        B, t_avg = 1, 4 + sum(len(t["raw"]) for t in trace) / max(1, 2 * len(trace))
+    ms_dec = elapsed / dec_steps * 1e3
+    step_bytes = decode_bytes_per_step(cfg, B, t_avg)
+    # dominant kernel (cross-attention over the encoder K/V, the largest per-step read): per-launch HIP
+    # events over an eager (non-graph) decode of the same batch shape, 16 steps
+    timer = KernelTimer("decode_attn_cross")
+    with timer:
+        if c4:
+            mel, _ = fe.extract(wavs[0], want_conv_input=False)
+            m.generate(mel, use_graph=False, language="zh", task="transcribe", max_new_tokens=16)
+        else:
+            m.generate(mel_long[:, :, :3000], use_graph=False, return_timestamps=True, language="zh",
+                       task="transcribe", max_new_tokens=16)
+    ks = timer.summary()
+    if rank == 0:
+        value = units_per_step * args.steps * world / elapsed
+        roof = None
+        if ks is not None:
+            achieved = ks["rate"] / 1e9
+            roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                        frac=round(achieved / PEAK_HBM_GBS, 4), traffic=None,
+                        kernel="decode_attn_kernel (cross-attention over the per-layer encoder K/V cache)",
+                        bytes_per_launch=int(ks["avg_work"]), avg_launch_ms=round(ks["avg_ms"], 5),
+                        launches_timed=ks["launches"])
+        out_d = {
+            "metric": ("pseudo-labelling greedy transcription utterances/sec (30 s clips)" if c4 else
+                       "long-form transcription speed (audio seconds per wall second)"),
+            "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (sines + noise, random-init large-v2 weights)" + (
+                "; eos suppressed -> fixed tokens per clip" if c4 else ""),
+            "config": {"workload": (f"c4: whisper-large-v2 batched greedy, {args.batch} x 30 s clips per step, "
+                                    f"{args.new_tokens} new tokens" if c4 else
+                                    f"c5: whisper-large-v2 long-form, {args.seconds:.0f} s recording, timestamps, "
+                                    f"<= {args.new_tokens} new tokens per window"),
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch, "parallelism":
+                       f"replicas{world}"},
+            "decode_steps": dec_steps, "ms_per_decode_step": round(ms_dec, 4),
+            "decode_step_hbm_frac": round(step_bytes / (ms_dec * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+        if not c4:
+            out_d["windows"] = len(trace)
+            out_d["real_time_factor"] = round(elapsed / args.steps / args.seconds, 5)
+        print(json.dumps(out_d), flush=True)
+    if pg is not None:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5"])
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--new-tokens", type=int, default=224, help="c4/c5: new tokens per clip / window")
+    ap.add_argument("--seconds", type=float, default=1800.0, help="c5: recording length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-teacher-fwd", action="store_true")
     args = ap.parse_args()
-    if args.batch is None:
-        args.batch = 64 if args.config == "c3" else 32
+    dflt = {"c3": (64, 10, 3), "c2": (32, 10, 3), "c4": (128, 4, 1), "c5": (1, 1, 1)}[args.config]
+    args.batch = dflt[0] if args.batch is None else args.batch
+    args.steps = dflt[1] if args.steps is None else args.steps
+    args.warmup = dflt[2] if args.warmup is None else args.warmup
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -168,6 +300,10 @@ def main():
         else:
             torch.distributed.init_process_group("nccl", device_id=device)
         pg = torch.distributed.group.WORLD
+
+    if args.config in ("c4", "c5"):
+        run_decode(args, device, rank, world, pg)
+        return
 
     from tw.distill import DistillationTrainer
     from tw.feature_extraction import WhisperFeatureExtractor

@@ -79,6 +79,12 @@ int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, int logits_
  * wav [B][480000] fp32 -> mel_out [B][80][3000] fp32 and optional conv1 input [B][3002][80] bf16. */
 int tw_logmel(const float* wav, int B, const float* basis, const int* mel_start, const float* mel_w, float* mel_out,
               void* conv_in, void* workspace /* B uint32 */, tw_stream_t stream);
+/* Same front end over clips of any length (long-form inputs: HF __call__(truncation=False,
+ * padding="longest"), run_eval.py:572-581): wav [B][n_samples] fp32 (shorter clips zero-padded to the
+ * longest, as HF pads) -> mel_out [B][80][n_samples/160], conv_in [B][n_samples/160 + 2][80] bf16.
+ * n_samples must exceed 200 (the reflect pad).  tw_logmel == tw_logmel_len(n_samples = 480000). */
+int tw_logmel_len(const float* wav, int B, int64_t n_samples, const float* basis, const int* mel_start,
+                  const float* mel_w, float* mel_out, void* conv_in, void* workspace, tw_stream_t stream);
 int tw_mel_to_conv_input(const float* mel, void* xt, int B, int nmel, int T, tw_stream_t stream);
 
 /* Decoder token + learned position embedding (HF modeling_whisper.py:736,754-761) and its

@@ -55,15 +55,17 @@ def pad_or_trim(wav: np.ndarray, n: int = N_SAMPLES) -> np.ndarray:
     return out
 
 
-def log_mel(wav: np.ndarray) -> np.ndarray:
-    """One clip -> [80, 3000] float64 (then compared against float32 outputs)."""
-    x = pad_or_trim(wav)
+def log_mel(wav: np.ndarray, n: int = N_SAMPLES) -> np.ndarray:
+    """One clip padded / trimmed to n samples -> [80, n // 160] float64 (then compared against float32
+    outputs).  n = 480 000 is the 30 s call; the long-form call (HF __call__(truncation=False,
+    padding="longest"), run_eval.py:572-581) passes n = the batch's longest clip."""
+    x = pad_or_trim(wav, n)
     xp = np.pad(x, (N_FFT // 2, N_FFT // 2), mode="reflect")
-    n_frames = 1 + (xp.shape[0] - N_FFT) // HOP          # 3001
+    n_frames = 1 + (xp.shape[0] - N_FFT) // HOP          # 3001 for 30 s
     idx = np.arange(N_FFT)[None, :] + HOP * np.arange(n_frames)[:, None]
     win = 0.5 - 0.5 * np.cos(2.0 * np.pi * np.arange(N_FFT) / N_FFT)   # periodic Hann
     spec = np.fft.rfft(xp[idx] * win[None, :], axis=1)     # [3001, 201]
-    power = (spec.real ** 2 + spec.imag ** 2)[:-1]          # drop last frame -> [3000, 201]
+    power = (spec.real ** 2 + spec.imag ** 2)[:-1]          # drop last frame -> [n // 160, 201]
     mel = power @ mel_filter_bank()                         # [3000, 80]
     log_spec = np.log10(np.maximum(mel, 1e-10)).T           # [80, 3000]
     log_spec = np.maximum(log_spec, log_spec.max() - 8.0)
@@ -72,6 +74,21 @@ def log_mel(wav: np.ndarray) -> np.ndarray:
 
 def log_mel_batch(wavs) -> np.ndarray:
     return np.stack([log_mel(w) for w in wavs]).astype(np.float32)
+
+
+def log_mel_longest(wavs):
+    """HF __call__(truncation=False, padding="longest", return_attention_mask=True): every clip zero-padded
+    to the longest one -> (features [B, 80, n // 160] float32, attention mask [B, n // 160] int: one
+    entry per hop of real samples, the sample mask rescaled by [::160] and trimmed to the frame count)."""
+    n = max(len(w) for w in wavs)
+    feats = np.stack([log_mel(w, n) for w in wavs]).astype(np.float32)
+    nfr = n // HOP
+    mask = np.zeros((len(wavs), nfr), dtype=np.int64)
+    for i, w in enumerate(wavs):
+        sm = np.zeros(n, dtype=np.int64)
+        sm[:len(w)] = 1
+        mask[i] = sm[::HOP][:nfr]
+    return feats, mask
 
 
 def synthetic_clip(i: int, seconds: float = 30.0) -> np.ndarray:

@@ -150,3 +150,8 @@ __device__ __forceinline__ uint32_t f2ord(float f) {
 __device__ __forceinline__ float ord2f(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
+
+// Per-device scratch block (gemm.hip): grown outside stream capture only, never freed (a captured graph
+// may hold an older block); users on one stream are ordered, so they may share it.  nullptr when it
+// cannot grow (e.g. during capture): callers fall back to a path without scratch.
+void* tw_device_workspace(hipStream_t stream, size_t bytes);

@@ -26,6 +26,7 @@ namespace {
 
 constexpr int DA_THREADS = 256;
 constexpr int DA_MAX_TK = 2048;
+constexpr int DA_SPLIT = 128;     // keys per workgroup of the split (flash-decoding) variant
 
 struct DecP {
   const void* q; int64_t sqb;
@@ -38,18 +39,18 @@ struct DecP {
 };
 
 // lane = (key slot ks = lane >> 3, 8-element chunk ch = lane & 7); a wave covers 8 keys per step.
-// E = bf16 (autocast path) or float (fp32 path: exact expf, no rounding of the output)
+// E = bf16 (autocast path) or float (fp32 path: exact expf, no rounding of the output).
+// The body attends keys [lo, hi).  part == nullptr: normalise and store O.  Otherwise (split over keys,
+// flash-decoding) store the chunk's unnormalised o[64], its max m (log2 domain) and sum l to part[0..65]
+// for decode_attn_combine_kernel.
 template <typename E>
-__global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
+__device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, int lo, int hi, float* part) {
   __shared__ float sc[DA_MAX_TK];
   __shared__ float red[DA_THREADS / 64][64];
   __shared__ float red_l[DA_THREADS / 64];
   __shared__ float red_m[DA_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ks = lane >> 3, ch = lane & 7;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
-  if (p.tk_dev) p.Tk += *p.tk_dev;
-  if (p.Tk > DA_MAX_TK) p.Tk = DA_MAX_TK;
   constexpr bool F32 = sizeof(E) == 4;
   const E* qb = (const E*)p.q + b * p.sqb + h * 64 + ch * 8;
   const E* kb = (const E*)p.k + b * p.skb + h * 64 + ch * 8;
@@ -58,10 +59,10 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
   load8(qb, qv);
   // pass 1: scores (log2 domain) -> LDS, running max
   float mx = -INFINITY;
-  for (int k0 = wave * 8; k0 < p.Tk; k0 += DA_THREADS / 8) {
+  for (int k0 = lo + wave * 8; k0 < hi; k0 += DA_THREADS / 8) {
     const int key = k0 + ks;
     float s = 0.f;
-    if (key < p.Tk) {
+    if (key < hi) {
       float t[8];
       load8(kb + (int64_t)key * p.ldk, t);
 #pragma unroll
@@ -70,9 +71,9 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if (key < p.Tk) {
+    if (key < hi) {
       s *= p.c;
-      if (ch == 0) sc[key] = s;
+      if (ch == 0) sc[key - lo] = s;
       mx = fmaxf(mx, s);
     }
   }
@@ -85,10 +86,10 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
   // pass 2: p = exp2(s - m), l = sum p, o = sum p * V
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float l = 0.f;
-  for (int k0 = wave * 8; k0 < p.Tk; k0 += DA_THREADS / 8) {
+  for (int k0 = lo + wave * 8; k0 < hi; k0 += DA_THREADS / 8) {
     const int key = k0 + ks;
-    if (key < p.Tk) {
-      const float pe = F32 ? exp2f(sc[key] - m) : __builtin_amdgcn_exp2f(sc[key] - m);
+    if (key < hi) {
+      const float pe = F32 ? exp2f(sc[key - lo] - m) : __builtin_amdgcn_exp2f(sc[key - lo] - m);
       float t[8];
       load8(vb + (int64_t)key * p.ldv, t);
 #pragma unroll
@@ -117,8 +118,64 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
       acc += red[w][tid];
       lt += red_l[w];
     }
-    from_f32(((E*)p.o)[b * p.sob + h * 64 + tid], acc / lt);
+    if (part) {
+      part[tid] = acc;
+      if (tid == 0) {
+        part[64] = m;
+        part[65] = lt;
+      }
+    } else {
+      from_f32(((E*)p.o)[b * p.sob + h * 64 + tid], acc / lt);
+    }
   }
+}
+
+template <typename E>
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  int tk = p.Tk + (p.tk_dev ? *p.tk_dev : 0);
+  if (tk > DA_MAX_TK) tk = DA_MAX_TK;
+  decode_attn_body<E>(p, b, h, 0, tk, nullptr);
+}
+
+// split over keys (few (clip, head) pairs: batch-1 long-form): blockIdx.y = chunk of S keys; chunks past
+// the effective Tk store an empty partial (m = -inf, l = 0)
+template <typename E>
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, int S, float* ws) {
+  const int bh = blockIdx.x, c = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  int tk = p.Tk + (p.tk_dev ? *p.tk_dev : 0);
+  if (tk > DA_MAX_TK) tk = DA_MAX_TK;
+  float* part = ws + ((int64_t)bh * gridDim.y + c) * 66;
+  const int lo = c * S, hi = min(tk, lo + S);
+  if (lo >= hi) {
+    if (threadIdx.x < 64) part[threadIdx.x] = 0.f;
+    if (threadIdx.x == 0) {
+      part[64] = -INFINITY;
+      part[65] = 0.f;
+    }
+    return;
+  }
+  decode_attn_body<E>(p, b, h, lo, hi, part);
+}
+
+// O = sum_c 2^(m_c - M) o_c / sum_c 2^(m_c - M) l_c over the chunks of one (clip, head), in chunk order
+template <typename E>
+__global__ __launch_bounds__(64) void decode_attn_combine_kernel(DecP p, int nchunk, const float* ws) {
+  const int bh = blockIdx.x, tid = threadIdx.x;
+  const int b = bh / p.H, h = bh % p.H;
+  const float* part = ws + (int64_t)bh * nchunk * 66;
+  float M = -INFINITY;
+  for (int c = 0; c < nchunk; ++c) M = fmaxf(M, part[c * 66 + 64]);
+  float acc = 0.f, lt = 0.f;
+  for (int c = 0; c < nchunk; ++c) {
+    const float mc = part[c * 66 + 64];
+    if (mc == -INFINITY) continue;
+    const float w = sizeof(E) == 4 ? exp2f(mc - M) : __builtin_amdgcn_exp2f(mc - M);
+    acc = fmaf(w, part[c * 66 + tid], acc);
+    lt = fmaf(w, part[c * 66 + 65], lt);
+  }
+  from_f32(((E*)p.o)[b * p.sob + h * 64 + tid], acc / lt);
 }
 
 struct SelP {
@@ -558,6 +615,18 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   p.v = v; p.ldv = ldv; p.svb = svb;
   p.o = o; p.sob = sob;
   p.H = H; p.Tk = Tk; p.tk_dev = tk_dev; p.c = scale * 1.4426950408889634f;
+  // fewer (clip, head) pairs than CUs over a long fixed key range (batch-1 long-form cross-attention):
+  // split the keys into chunks of DA_SPLIT over the grid's y dimension, then combine
+  const int nchunk = (Tk + DA_SPLIT - 1) / DA_SPLIT;
+  if (!tk_dev && B * H < 256 && nchunk >= 2) {
+    float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
+    if (ws) {
+      TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws);
+      TW_LAUNCH_DT(dtype, decode_attn_combine_kernel, dim3(B * H), dim3(64), p, nchunk, ws);
+      TW_CHECK_LAUNCH();
+      return TW_OK;
+    }
+  }
   TW_LAUNCH_DT(dtype, decode_attn_kernel, dim3(B * H), dim3(DA_THREADS), p);
   TW_CHECK_LAUNCH();
   return TW_OK;

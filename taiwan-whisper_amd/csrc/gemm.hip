@@ -638,6 +638,9 @@ void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
 
 }  // namespace
 
+// the same per-device block for other stream-ordered scratch users (decode attention split partials)
+void* tw_device_workspace(hipStream_t stream, size_t bytes) { return splitk_workspace(stream, bytes); }
+
 extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
                             void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
                             int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,

@@ -4,6 +4,10 @@
 // frames every 160 samples, |DFT|^2 (201 bins), slaney mel (80), log10(max(x,1e-10)),
 // max(x, clip_max - 8), (x + 4) / 4.
 //
+// Clips are n_samples long (480 000 = 30 s for the training / short-form path; any length for the
+// long-form path, HF __call__(truncation=False, padding="longest"), run_eval.py:572-581), giving
+// n_samples / 160 frames.
+//
 // Kernel 1: one workgroup = 64 frames of one clip.  The 10 480 samples the frames span
 // are staged in LDS (coalesced reads, reflect padding resolved there); the windowed DFT
 // runs on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32) against a [400][416] basis with the
@@ -16,7 +20,7 @@
 
 namespace {
 
-constexpr int NFFT = 400, HOP = 160, NBIN = 201, NMEL = 80, NFR = 3000, NS = 480000;
+constexpr int NFFT = 400, HOP = 160, NBIN = 201, NMEL = 80;
 constexpr int FPB = 64;                        // frames per block
 constexpr int NSAMP = (FPB - 1) * HOP + NFFT;  // 10480
 constexpr int NCOL = 416;                      // 13 tiles cos + 13 tiles sin
@@ -27,7 +31,7 @@ typedef __attribute__((ext_vector_type(4))) float v4f;
 __global__ __launch_bounds__(256, 1) void logmel_kernel(const float* __restrict__ wav, const float* __restrict__ basis,
                                                         const int* __restrict__ mel_start,
                                                         const float* __restrict__ mel_w, float* __restrict__ out,
-                                                        uint32_t* __restrict__ clip_max) {
+                                                        uint32_t* __restrict__ clip_max, int64_t NS, int NFR) {
   __shared__ float samp[NSAMP];
   __shared__ float pw[FPB][NBIN + 3];
   const int b = blockIdx.y;
@@ -36,7 +40,7 @@ __global__ __launch_bounds__(256, 1) void logmel_kernel(const float* __restrict_
   const int lane = lane_id(), wave = threadIdx.x >> 6;
   // stage samples of padded positions [f0*HOP, f0*HOP + NSAMP) with reflect padding
   for (int j = threadIdx.x; j < NSAMP; j += 256) {
-    int i = f0 * HOP + j - NFFT / 2;
+    int64_t i = (int64_t)f0 * HOP + j - NFFT / 2;
     if (i < 0) i = -i;
     if (i >= NS) i = 2 * (NS - 1) - i;
     samp[j] = (i >= 0 && i < NS) ? x[i] : 0.f;
@@ -111,16 +115,17 @@ __global__ __launch_bounds__(256, 1) void logmel_kernel(const float* __restrict_
 }
 
 __global__ void logmel_finalize_kernel(float* __restrict__ mel, const uint32_t* __restrict__ clip_max,
-                                       bf16* __restrict__ xt, int B) {
+                                       bf16* __restrict__ xt, int B, int NFR) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = (int64_t)B * NMEL * NFR;
   if (i < n) {
-    const int b = i / (NMEL * NFR);
+    const int b = i / ((int64_t)NMEL * NFR);
     const float floor_v = ord2f(clip_max[b]) - 8.f;
     const float v = (fmaxf(mel[i], floor_v) + 4.f) / 4.f;
     mel[i] = v;
     if (xt) {
-      const int m = (i / NFR) % NMEL, t = i % NFR;
+      const int m = (i / NFR) % NMEL;
+      const int t = i % NFR;
       xt[((int64_t)b * (NFR + 2) + t + 1) * NMEL + m] = f2bf(v);
     }
   }
@@ -133,18 +138,25 @@ __global__ void logmel_finalize_kernel(float* __restrict__ mel, const uint32_t* 
 
 }  // namespace
 
-// wav [B][480000] f32 (already padded/truncated); basis [400][416]; mel_start [80]; mel_w [80][32]
-// mel_out [B][80][3000] f32; conv_in (optional) [B][3002][80] bf16; workspace >= B uint32
-extern "C" int tw_logmel(const float* wav, int B, const float* basis, const int* mel_start, const float* mel_w,
-                         float* mel_out, void* conv_in, void* workspace, hipStream_t stream) {
+// wav [B][n_samples] f32 (already padded/truncated); basis [400][416]; mel_start [80]; mel_w [80][32]
+// mel_out [B][80][n_samples/160] f32; conv_in (optional) [B][n_samples/160 + 2][80] bf16; workspace >= B uint32
+extern "C" int tw_logmel_len(const float* wav, int B, int64_t n_samples, const float* basis, const int* mel_start,
+                             const float* mel_w, float* mel_out, void* conv_in, void* workspace, hipStream_t stream) {
   if (B <= 0) return TW_OK;
+  if (n_samples < NFFT / 2 + 1 || n_samples / HOP > (1 << 30) / NMEL) return TW_EINVAL;   // reflect pad needs > 200
+  const int nfr = (int)(n_samples / HOP);
   uint32_t* cm = (uint32_t*)workspace;
   if (hipMemsetAsync(cm, 0, sizeof(uint32_t) * B, stream) != hipSuccess) return TW_EHIP;
-  hipLaunchKernelGGL(logmel_kernel, dim3((NFR + FPB - 1) / FPB, B), dim3(256), 0, stream, wav, basis, mel_start, mel_w,
-                     mel_out, cm);
-  const int64_t n = (int64_t)B * NMEL * NFR;
+  hipLaunchKernelGGL(logmel_kernel, dim3((nfr + FPB - 1) / FPB, B), dim3(256), 0, stream, wav, basis, mel_start, mel_w,
+                     mel_out, cm, n_samples, nfr);
+  const int64_t n = (int64_t)B * NMEL * nfr;
   hipLaunchKernelGGL(logmel_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, mel_out, cm, (bf16*)conv_in,
-                     B);
+                     B, nfr);
   TW_CHECK_LAUNCH();
   return TW_OK;
+}
+
+extern "C" int tw_logmel(const float* wav, int B, const float* basis, const int* mel_start, const float* mel_w,
+                         float* mel_out, void* conv_in, void* workspace, hipStream_t stream) {
+  return tw_logmel_len(wav, B, 480000, basis, mel_start, mel_w, mel_out, conv_in, workspace, stream);
 }

@@ -25,6 +25,7 @@ SIGNATURES = {
                     I32, I32, F32, P, P],
     "tw_kl_ce": [P, P, I64, I32, P, I64, I32, F32, F32, F32, P, F32, P, P, P, P],
     "tw_logmel": [P, I32, P, P, P, P, P, P, P],
+    "tw_logmel_len": [P, I32, I64, P, P, P, P, P, P, P],
     "tw_mel_to_conv_input": [P, P, I32, I32, I32, P],
     "tw_embed_fwd": [P, P, I32, P, I32, P, I32, I32, I32, I32, I32, P],
     "tw_embed_bwd": [P, P, P, I32, I32, P],

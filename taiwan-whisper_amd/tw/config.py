@@ -59,6 +59,31 @@ class WhisperConfig:
         return f"WhisperConfig(d_model={self.d_model}, enc={self.encoder_layers}, dec={self.decoder_layers})"
 
 
+def _dims(d, enc, dec, heads, ffn):
+    return dict(d_model=d, encoder_layers=enc, decoder_layers=dec, encoder_attention_heads=heads,
+                decoder_attention_heads=heads, encoder_ffn_dim=ffn, decoder_ffn_dim=ffn)
+
+
+# architecture dims of the checkpoints the reference names (openai/whisper-* config.json; distil-32-2 is
+# create_student_model.py with --decoder_layers 2 from large-v2)
+MODEL_DIMS = {
+    "tiny": _dims(384, 4, 4, 6, 1536),
+    "base": _dims(512, 6, 6, 8, 2048),
+    "small": _dims(768, 12, 12, 12, 3072),
+    "medium": _dims(1024, 24, 24, 16, 4096),
+    "large-v2": _dims(1280, 32, 32, 20, 5120),
+    "distil-32-2": _dims(1280, 32, 2, 20, 5120),
+}
+
+# openai/whisper-large-v2 generation_config.json suppress_tokens (the multilingual checkpoints' list)
+LARGE_V2_SUPPRESS = [1, 2, 7, 8, 9, 10, 14, 25, 26, 27, 28, 29, 31, 58, 59, 60, 61, 62, 63, 90, 91, 92, 93,
+                     359, 503, 522, 542, 873, 893, 902, 918, 922, 931, 1350, 1853, 1982, 2460, 2627, 3246,
+                     3253, 3268, 3536, 3846, 3961, 4183, 4667, 6585, 6647, 7273, 9061, 9383, 10428, 10929,
+                     11938, 12033, 12331, 12562, 13793, 14157, 14635, 15265, 15618, 16553, 16604, 18362,
+                     18956, 20075, 21675, 22520, 26130, 26161, 26435, 28279, 29464, 31650, 32302, 32470,
+                     36865, 42863, 47425, 49870, 50254, 50258, 50358, 50359, 50360, 50361, 50362]
+
+
 GEN_DEFAULTS = dict(
     decoder_start_token_id=50258, eos_token_id=50257, pad_token_id=50257, bos_token_id=50257,
     no_timestamps_token_id=50363, max_length=448, num_beams=1, suppress_tokens=[], begin_suppress_tokens=[220, 50257],

@@ -109,14 +109,18 @@ def synthetic_label_lists(B, seed=0, prompt_fraction=0.2, min_len=32, max_len=44
     return out
 
 
-def synthetic_audio(B, seed=0, seconds=30.0, device="cuda"):
-    """x_i(t) = 0.5 sin(2π(220 + 37 i) t) + 0.01 N(0,1) as a [B, 480000] fp32 device tensor."""
+def synthetic_audio(B, seed=0, seconds=30.0, device="cuda", length=480000):
+    """x_i(t) = 0.5 sin(2π(220 + 37 i) t) + 0.01 N(0,1) as a [B, length] fp32 device tensor (zero-padded /
+    truncated to `length` samples: 480 000 = the 30 s window; pass length=None for the clip's own
+    length, e.g. a long-form input)."""
     n = int(seconds * 16000)
+    length = n if length is None else length
     t = torch.arange(n, device=device, dtype=torch.float64) / 16000.0
     g = torch.Generator(device=device).manual_seed(1234 + seed)
     f = 220.0 + 37.0 * torch.arange(B, device=device, dtype=torch.float64)[:, None]
     x = 0.5 * torch.sin(2 * math.pi * f * t[None, :]) + 0.01 * torch.randn(B, n, generator=g, device=device,
                                                                            dtype=torch.float64)
-    out = torch.zeros(B, 480000, dtype=torch.float32, device=device)
-    out[:, :n] = x.float()[:, :480000]
+    out = torch.zeros(B, length, dtype=torch.float32, device=device)
+    k = min(n, length)
+    out[:, :k] = x[:, :k].float()
     return out

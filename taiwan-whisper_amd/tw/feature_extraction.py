@@ -96,31 +96,57 @@ class WhisperFeatureExtractor:
     def mel_filters(self):
         return mel_filters().astype(np.float32)
 
-    def pad_waveforms(self, raw_speech) -> torch.Tensor:
-        """padding='max_length' to 480 000 samples with 0.0, truncation=True (HF __call__)."""
+    @staticmethod
+    def _as_list(raw_speech):
         if isinstance(raw_speech, (np.ndarray, torch.Tensor)) and getattr(raw_speech, "ndim", 1) == 1:
-            raw_speech = [raw_speech]
-        out = torch.zeros(len(raw_speech), N_SAMPLES, dtype=torch.float32)
+            return [raw_speech]
+        return list(raw_speech)
+
+    def pad_waveforms(self, raw_speech, n: int = N_SAMPLES) -> torch.Tensor:
+        """Zero-pad / truncate every clip to n samples (HF __call__: padding='max_length' to 480 000 with
+        truncation=True by default; n = the longest clip for padding='longest', truncation=False)."""
+        raw_speech = self._as_list(raw_speech)
+        out = torch.zeros(len(raw_speech), n, dtype=torch.float32)
         for i, w in enumerate(raw_speech):
-            w = torch.as_tensor(np.asarray(w, dtype=np.float32)).reshape(-1)[:N_SAMPLES]
+            w = torch.as_tensor(np.asarray(w, dtype=np.float32)).reshape(-1)[:n]
             out[i, : w.shape[0]] = w
         return out
 
     def extract(self, wav: torch.Tensor, want_conv_input: bool = True):
-        """wav: [B, 480000] fp32 (host or device) -> (mel [B,80,3000] fp32, conv_in [B,3002,80] bf16)."""
+        """wav: [B, n] fp32 (host or device) -> (mel [B,80,n//160] fp32, conv_in [B,n//160+2,80] bf16);
+        n = 480 000 for 30 s clips, any n > 200 for long-form inputs."""
         wav = wav.to(self.device, torch.float32).contiguous()
-        B = wav.shape[0]
+        B, n = wav.shape
+        nfr = n // HOP
         basis, start, w = self._tabs()
-        mel = torch.empty(B, N_MELS, N_FRAMES, dtype=torch.float32, device=self.device)
-        conv = torch.empty(B, N_FRAMES + 2, N_MELS, dtype=torch.bfloat16, device=self.device) if want_conv_input else None
+        mel = torch.empty(B, N_MELS, nfr, dtype=torch.float32, device=self.device)
+        conv = torch.empty(B, nfr + 2, N_MELS, dtype=torch.bfloat16, device=self.device) if want_conv_input else None
         ops.logmel(wav, basis, start, w, mel, conv)
         return mel, conv
 
-    def __call__(self, raw_speech, sampling_rate=None, return_tensors=None, **kw):
+    def __call__(self, raw_speech, sampling_rate=None, return_tensors=None, truncation=True, padding="max_length",
+                 return_attention_mask=None, **kw):
+        """HF WhisperFeatureExtractor.__call__ for the reference's two calls: the training default
+        (padding='max_length', truncation=True -> [B, 80, 3000]; run_distillation.py:1217) and the long-form
+        eval call (truncation=False, padding='longest', return_attention_mask=True -> [B, 80, n_max // 160]
+        plus a per-frame mask, run_eval.py:572-581)."""
         if sampling_rate is not None and sampling_rate != self.sampling_rate:
             raise ValueError(f"expected sampling_rate {self.sampling_rate}, got {sampling_rate}")
-        mel, conv = self.extract(self.pad_waveforms(raw_speech))
-        return _Features(mel, conv)
+        clips = self._as_list(raw_speech)
+        lens = [int(np.asarray(c).reshape(-1).shape[0]) for c in clips]
+        if padding == "longest":
+            n = max(lens) if not truncation else min(max(lens), N_SAMPLES)
+        elif padding in ("max_length", True, None):
+            n = N_SAMPLES if (truncation or max(lens) <= N_SAMPLES) else max(lens)
+        else:
+            raise NotImplementedError(f"padding={padding!r}")
+        mel, conv = self.extract(self.pad_waveforms(clips, n))
+        out = _Features(mel, conv)
+        if return_attention_mask:
+            nfr = n // HOP
+            frame = torch.arange(nfr) * HOP         # the sample mask rescaled by [::hop], trimmed to the frames
+            out["attention_mask"] = (frame[None, :] < torch.tensor(lens)[:, None]).to(torch.int32).to(self.device)
+        return out
 
     def pad(self, features: dict, padding="longest", return_tensors="pt", **kw):
         feats = features["input_features"]

@@ -159,15 +159,22 @@ def kl_ce(s_logits, t_logits, labels, V, n_valid, T=2.0, ce_w=0.8, kl_w=1.0, gra
 
 
 def logmel(wav, basis, mel_start, mel_w, mel_out, conv_in=None, workspace=None):
-    B = wav.shape[0]
-    assert wav.shape == (B, 480000) and wav.dtype == torch.float32 and wav.is_contiguous()
-    assert mel_out.shape == (B, 80, 3000) and mel_out.dtype == torch.float32
+    """wav [B, n] fp32 -> mel_out [B, 80, n // 160] (+ conv_in [B, n // 160 + 2, 80] bf16).  n = 480 000 is the
+    30 s path (tw_logmel); any other n > 200 is the long-form path (tw_logmel_len)."""
+    B, n = wav.shape
+    nfr = n // 160
+    assert wav.dtype == torch.float32 and wav.is_contiguous() and n > 200
+    assert mel_out.shape == (B, 80, nfr) and mel_out.dtype == torch.float32 and mel_out.is_contiguous()
     if conv_in is not None:
-        assert conv_in.shape == (B, 3002, 80) and conv_in.dtype == torch.bfloat16
+        assert conv_in.shape == (B, nfr + 2, 80) and conv_in.dtype == torch.bfloat16 and conv_in.is_contiguous()
     if workspace is None:
         workspace = torch.empty(B, dtype=torch.int32, device=wav.device)
-    call("tw_logmel", wav.data_ptr(), B, basis.data_ptr(), mel_start.data_ptr(), mel_w.data_ptr(),
-         mel_out.data_ptr(), _ptr(conv_in), workspace.data_ptr(), _stream())
+    if n == 480000:
+        call("tw_logmel", wav.data_ptr(), B, basis.data_ptr(), mel_start.data_ptr(), mel_w.data_ptr(),
+             mel_out.data_ptr(), _ptr(conv_in), workspace.data_ptr(), _stream())
+    else:
+        call("tw_logmel_len", wav.data_ptr(), B, n, basis.data_ptr(), mel_start.data_ptr(), mel_w.data_ptr(),
+             mel_out.data_ptr(), _ptr(conv_in), workspace.data_ptr(), _stream())
     return mel_out
 
 
@@ -295,8 +302,12 @@ def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_de
     _need(o, (B - 1) * sob + H * hd, "decode o")
     if tk_dev is not None:
         assert tk_dev.dtype == torch.int32 and tk_max is not None
-    call("tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb, o.data_ptr(), sob,
-         B, H, Tk, _ptr(tk_dev), hd, float(scale), _dt(q), _stream())
+    # algorithmic bytes (KernelTimer family "decode_attn_cross" / "decode_attn_self"): every K and V
+    # element of the rows attended once (self: the host does not know *tk_dev; tk_max bounds it)
+    work = 2 * B * rows * H * hd * q.element_size()
+    KernelTimer.wrap("decode_attn_self" if tk_dev is not None else "decode_attn_cross", work, lambda: call(
+        "tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb, o.data_ptr(), sob,
+        B, H, Tk, _ptr(tk_dev), hd, float(scale), _dt(q), _stream()))
     return o
 
 

@@ -78,6 +78,26 @@ def gen_mel(out):
     out["mel_filters"] = fe.mel_filters.astype(np.float32)
 
 
+def longform_clips():
+    """Two long-form clips of different lengths (47.3 s, 65 s: not a multiple of the hop)."""
+    return [logmel.synthetic_clip(6, 47.3), logmel.synthetic_clip(7, 65.0)]
+
+
+def gen_mel_long(out):
+    """HF long-form feature extraction as run_eval.py:572-581 calls it (truncation=False,
+    padding="longest", return_attention_mask=True)."""
+    from transformers import WhisperFeatureExtractor
+    fe = WhisperFeatureExtractor()
+    r = fe(longform_clips(), sampling_rate=16000, return_tensors="np", truncation=False, padding="longest",
+           return_attention_mask=True)
+    mel = r.input_features.astype(np.float32)
+    out["mel_sub"] = mel[:, :, ::10]
+    out["mel_rowsum"] = mel.sum(-1)
+    out["mel_max"] = mel.reshape(mel.shape[0], -1).max(-1)
+    out["shape"] = np.array(mel.shape)
+    out["attention_mask"] = np.asarray(r.attention_mask).astype(np.int8)
+
+
 def gen_micro(out):
     from transformers.modeling_outputs import BaseModelOutput
     cfg = CONFIGS["micro"]
@@ -423,7 +443,7 @@ def gen_cfg(case, out):
 def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
-    for name, fn in (("mel", gen_mel), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
+    for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
                      ("cfg_c3", lambda o: gen_cfg("c3", o))):

@@ -1,7 +1,8 @@
 """Greedy KV-cache decoding on the GPU, bf16-autocast path.
 
 * tw_decode_attn vs an fp64 softmax-attention reference (single query row per (b, h), strided
-  caches, Tk from 1 to 1500);
+  caches; B*H < 256 over >= 2 chunks of keys runs the split-key variant + combine, B*H >= 256 the
+  one-workgroup-per-row kernel; Tk from 1 to 2048);
 * tw_greedy_select vs torch (suppress / begin-suppress masks, ties -> lowest id, finished rows);
 * generate() KV cache vs a full recompute of the prefix with the same engine (every step);
 * generate() under bf16 autocast vs the bf16-autocast oracle (oracle/whisper_ref.Ref(amp=True), pinned to
@@ -32,7 +33,8 @@ def bf(x):
     return x.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("B,H,Tk", [(3, 2, 1), (2, 3, 5), (4, 20, 447), (2, 4, 1500), (1, 1, 2048)])
+@pytest.mark.parametrize("B,H,Tk", [(3, 2, 1), (2, 3, 5), (4, 20, 447), (2, 4, 1500), (1, 1, 2048), (1, 20, 1500),
+                                    (13, 20, 1500)])
 def test_decode_attn(B, H, Tk):
     from tw import ops
     g = torch.Generator().manual_seed(B * 131 + Tk)

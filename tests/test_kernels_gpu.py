@@ -512,6 +512,42 @@ def test_logmel_matches_oracle():
     assert (c[:, 1:3001].transpose(1, 2) - bf(mel.cpu()).float()).abs().max() == 0
 
 
+def test_logmel_longform_matches_oracle_and_hf():
+    """Long-form front end (tw_logmel_len through WhisperFeatureExtractor(truncation=False,
+    padding="longest", return_attention_mask=True), run_eval.py:572-581): two clips of 47.3 s and 65 s
+    (not a multiple of the hop) against the float64 oracle and HF's own output (mel_long.npz)."""
+    from conftest import load_golden
+    from oracle import logmel as ol
+    from tw.feature_extraction import WhisperFeatureExtractor
+    clips = [ol.synthetic_clip(6, 47.3), ol.synthetic_clip(7, 65.0)]
+    fe = WhisperFeatureExtractor(device=DEV)
+    r = fe(clips, sampling_rate=16000, truncation=False, padding="longest", return_attention_mask=True)
+    got = r.input_features.cpu().numpy()
+    ref, mask = ol.log_mel_longest(clips)
+    g = load_golden("mel_long")
+    assert got.shape == ref.shape == tuple(g["shape"])
+    err, err_hf = np.abs(got - ref).max(), np.abs(got[:, :, ::10] - g["mel_sub"]).max()
+    print(f"long-form log-mel max abs err vs oracle {err:.2e}, vs HF {err_hf:.2e}")
+    assert err < 1e-4 and err_hf < 1e-4
+    assert (r["attention_mask"].cpu().numpy() == g["attention_mask"]).all()
+    c = r.conv_input.float().cpu()
+    T = got.shape[-1]
+    assert c.shape == (2, T + 2, 80) and (c[:, 0] == 0).all() and (c[:, T + 1] == 0).all()
+    assert (c[:, 1:T + 1].transpose(1, 2) - bf(r.input_features.cpu()).float()).abs().max() == 0
+    # 30 s inputs through the generic entry are the fixed-size kernel's values bit for bit
+    w30 = torch.stack([torch.from_numpy(ol.pad_or_trim(x).astype(np.float32)) for x in clips]).to(DEV)
+    a, _ = fe.extract(w30)
+    from tw import ops
+    from tw.feature_extraction import mel_tables
+    basis, start, w = (t.to(DEV) for t in mel_tables())
+    b = torch.empty(2, 80, 3000, device=DEV)
+    lib_ws = torch.empty(2, dtype=torch.int32, device=DEV)
+    from tw._native import call
+    call("tw_logmel_len", w30.data_ptr(), 2, 480000, basis.data_ptr(), start.data_ptr(), w.data_ptr(), b.data_ptr(),
+         None, lib_ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(a, b)
+
+
 # ----------------------------------------------------------------------------- misc
 def test_embed_adamw_norm_shift():
     from tw import ops

@@ -27,6 +27,17 @@ def test_logmel_matches_hf():
     np.testing.assert_allclose(mel.max(axis=(1, 2)), g["mel_max"], atol=2e-4)
 
 
+def test_logmel_longform_matches_hf():
+    """Long-form call (run_eval.py:572-581: truncation=False, padding="longest", attention mask)."""
+    g = load_golden("mel_long")
+    clips = [logmel.synthetic_clip(6, 47.3), logmel.synthetic_clip(7, 65.0)]
+    mel, mask = logmel.log_mel_longest(clips)
+    assert tuple(g["shape"]) == mel.shape
+    np.testing.assert_allclose(mel[:, :, ::10], g["mel_sub"], atol=2e-4, rtol=0)
+    np.testing.assert_allclose(mel.max(axis=(1, 2)), g["mel_max"], atol=2e-4)
+    assert (mask == g["attention_mask"]).all()
+
+
 def test_collator_prompt_quirk():
     """SURVEY.md finding 3: student vs teacher decoder inputs with a prompt."""
     sot, zh, tr, nt = SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]
