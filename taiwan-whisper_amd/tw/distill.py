@@ -91,6 +91,11 @@ class DistillationTrainer:
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.bucket = dp_bucket_mb * (1 << 20) // 4
+        # DDP mean (torch Reducer, no comm hook): every rank's gradient is multiplied by fp32(1/world) as it
+        # enters its bucket, then the buckets are SUM-all-reduced.  For a power-of-two world the factor is
+        # exact and commutes with every rounding of the backward, so it is folded into the loss gradient
+        # (no extra pass); otherwise each slice is scaled right before its all-reduce, as DDP does.
+        self.fold_world = self.world & (self.world - 1) == 0
         set_trainable_like_reference(student, freeze_encoder, freeze_decoder, freeze_embed_positions)
         self.train_encoder = not freeze_encoder
         self.freeze_encoder, self.freeze_decoder = freeze_encoder, freeze_decoder
@@ -173,7 +178,7 @@ class DistillationTrainer:
         F.count_valid(lab, self.nvalid)
         dlogits = torch.empty_like(ls)
         out3, _ = F.kl_ce(ls, lt, lab, s.config.vocab_size, self.nvalid, T=T, ce_w=0.8, kl_w=self.kl_weight,
-                          grad_scale=1.0 / (self.accum * self.world), dlogits=dlogits)
+                          grad_scale=1.0 / (self.accum * (self.world if self.fold_world else 1)), dlogits=dlogits)
         del lt
         d_enc = torch.zeros(B * Tk, s.config.d_model, dtype=torch.float32, device=s.device) \
             if self.train_encoder else None
@@ -208,8 +213,10 @@ class DistillationTrainer:
     def _launch(self, lo, hi):
         g = self.s.grad
         for a in range(lo, hi, self.bucket):
-            self._pending.append(torch.distributed.all_reduce(g[a: min(hi, a + self.bucket)], group=self.pg,
-                                                              async_op=True))
+            sl = g[a: min(hi, a + self.bucket)]
+            if not self.fold_world:
+                sl.mul_(1.0 / self.world)          # DDP: grad * fp32(1/world) into the bucket, then SUM
+            self._pending.append(torch.distributed.all_reduce(sl, group=self.pg, async_op=True))
         self._reduced.append((lo, hi))
 
     def _grad_ready(self, prefix):
@@ -218,8 +225,8 @@ class DistillationTrainer:
             self._launch(*r)
 
     def all_reduce_grads(self):
-        """DDP mean over ranks (the 1/world factor is already folded into the loss gradient):
-        bucketed SUM all-reduce of the flat fp32 gradient over RCCL.  Ranges whose exchange already
+        """DDP mean over ranks: bucketed SUM all-reduce of the flat fp32 gradient over RCCL, each rank's
+        gradient scaled by 1/world first (folded into the loss gradient for power-of-two worlds).  Ranges whose exchange already
         started during the backward (per finished layer) are skipped; the rest (embeddings, final
         LayerNorm, ...) is launched now, then everything is waited for."""
         if self.world == 1:

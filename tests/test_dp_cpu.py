@@ -1,9 +1,10 @@
 """Data-parallel semantics on CPU with gloo, world_size 2 (no GPU needed).
 
 1. The product's gradient exchange (`DistillationTrainer.all_reduce_grads`, bucketed async SUM of
-   the flat fp32 gradient with the 1/world factor folded into the loss gradient; per-layer ranges
-   launched early during the backward, the remainder at the end) equals the DDP mean of per-rank
-   gradients, for bucket sizes and early ranges that split the buffer unevenly.
+   the flat fp32 gradient; per-layer ranges launched early during the backward, the remainder at the
+   end) equals the DDP mean of per-rank gradients, for bucket sizes and early ranges that split the
+   buffer unevenly: world 2 (1/world folded into the loss gradient, exact) and world 3 (each slice
+   scaled by fp32(1/3) before its SUM, torch Reducer's order -- bit-exact against that recipe).
 2. SURVEY.md §8(e) semantics on the oracle step: 2 ranks x half batch with DDP mean == 1 process
    accumulating the two halves with loss / 2 each (per-rank token normalisation kept).
 """
@@ -32,6 +33,7 @@ def _init(rank, world, port):
 
 
 def _worker_allreduce(rank, world, port, out):
+    fold = world & (world - 1) == 0
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "taiwan-whisper_amd"))
     from tw.distill import DistillationTrainer
@@ -47,8 +49,9 @@ def _worker_allreduce(rank, world, port, out):
     st = Stub()
     st.s = Stub()
     st.bw = Stub()
-    st.s.grad = local / world            # the trainer folds 1/world into grad_scale
-    st.world, st.pg, st.bucket = world, dist.group.WORLD, 3001
+    # power-of-two world: the trainer folds 1/world into the loss gradient; otherwise the exchange scales
+    st.s.grad = local / world if fold else local.clone()
+    st.world, st.pg, st.bucket, st.fold_world = world, dist.group.WORLD, 3001, fold
     st._launch = types.MethodType(DistillationTrainer._launch, st)
     # two "layers" finished during the backward start their exchange early (out of order, uneven
     # sizes); all_reduce_grads then covers the gaps and waits for everything
@@ -61,15 +64,23 @@ def _worker_allreduce(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_allreduce_is_ddp_mean():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_allreduce_is_ddp_mean(world):
     port = _free_port()
     out = mp.Manager().dict()
     mp.spawn(_worker_allreduce, args=(world, port, out), nprocs=world, join=True)
     n = 10_007
-    mean = sum(torch.randn(n, generator=torch.Generator().manual_seed(r)) for r in range(world)) / world
+    g = [torch.randn(n, generator=torch.Generator().manual_seed(r)) for r in range(world)]
+    # torch DDP (Reducer::mark_variable_ready_dense without a comm hook): bucket = grad * (1/world), SUM
+    scaled = [x * (1.0 / world) for x in g]
     for r in range(world):
-        assert torch.allclose(out[r], mean, atol=1e-6)
+        got = out[r]
+        # every rank holds the same bits; vs the DDP recipe: a 3-term fp32 sum in some order (1 ulp)
+        assert torch.equal(got, out[0])
+        assert torch.allclose(got, scaled[0] + scaled[1] + (scaled[2] if world == 3 else 0), rtol=2e-7, atol=1e-7)
+        if world == 3:
+            # not the folded variant's bits in general (a rank-local 1/3 before vs after rounding)
+            assert torch.allclose(got, sum(g) / 3, rtol=1e-6, atol=1e-6)
 
 
 def _worker_oracle(rank, world, port, out):
