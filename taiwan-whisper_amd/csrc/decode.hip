@@ -22,11 +22,14 @@
 //  * tw_token_logprob: log-softmax of a raw logits row at one id (WhisperNoSpeechDetection).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int DA_THREADS = 256;
 constexpr int DA_MAX_TK = 2048;
-constexpr int DA_SPLIT = 128;     // keys per workgroup of the split (flash-decoding) variant
+constexpr int DA_SPLIT = 128;
+constexpr int DA_U = 4;           // key sub-steps per wave iteration (loads in flight per lane)     // keys per workgroup of the split (flash-decoding) variant
 
 struct DecP {
   const void* q; int64_t sqb;
@@ -57,24 +60,32 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
   const E* vb = (const E*)p.v + b * p.svb + h * 64 + ch * 8;
   float qv[8];
   load8(qb, qv);
-  // pass 1: scores (log2 domain) -> LDS, running max
+  // pass 1: scores (log2 domain) -> LDS, running max.  A wave takes 8 keys x DA_U sub-steps per iteration
+  // (keys k0 + 8u + ks): DA_U independent 16-B loads per lane in flight before the reductions.
   float mx = -INFINITY;
-  for (int k0 = lo + wave * 8; k0 < hi; k0 += DA_THREADS / 8) {
-    const int key = k0 + ks;
-    float s = 0.f;
-    if (key < hi) {
-      float t[8];
-      load8(kb + (int64_t)key * p.ldk, t);
+  for (int k0 = lo + wave * 8 * DA_U; k0 < hi; k0 += DA_THREADS / 8 * DA_U) {
+    float t[DA_U][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s = fmaf(qv[j], t[j], s);
+    for (int u = 0; u < DA_U; ++u) {
+      const int key = k0 + 8 * u + ks;
+      if (key < hi) load8(kb + (int64_t)key * p.ldk, t[u]);
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    if (key < hi) {
-      s *= p.c;
-      if (ch == 0) sc[key - lo] = s;
-      mx = fmaxf(mx, s);
+#pragma unroll
+    for (int u = 0; u < DA_U; ++u) {
+      const int key = k0 + 8 * u + ks;
+      float sv = 0.f;
+      if (key < hi) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sv = fmaf(qv[j], t[u][j], sv);
+      }
+      sv += __shfl_xor(sv, 1, 64);
+      sv += __shfl_xor(sv, 2, 64);
+      sv += __shfl_xor(sv, 4, 64);
+      if (key < hi) {
+        sv *= p.c;
+        if (ch == 0) sc[key - lo] = sv;
+        mx = fmaxf(mx, sv);
+      }
     }
   }
   mx = wave_max(mx);
@@ -83,18 +94,25 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
   float m = red_m[0];
 #pragma unroll
   for (int w = 1; w < DA_THREADS / 64; ++w) m = fmaxf(m, red_m[w]);
-  // pass 2: p = exp2(s - m), l = sum p, o = sum p * V
+  // pass 2: p = exp2(s - m), l = sum p, o = sum p * V (same key order within each lane slot)
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float l = 0.f;
-  for (int k0 = lo + wave * 8; k0 < hi; k0 += DA_THREADS / 8) {
-    const int key = k0 + ks;
-    if (key < hi) {
-      const float pe = F32 ? exp2f(sc[key - lo] - m) : __builtin_amdgcn_exp2f(sc[key - lo] - m);
-      float t[8];
-      load8(vb + (int64_t)key * p.ldv, t);
+  for (int k0 = lo + wave * 8 * DA_U; k0 < hi; k0 += DA_THREADS / 8 * DA_U) {
+    float t[DA_U][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fmaf(pe, t[j], o[j]);
-      if (ch == 0) l += pe;
+    for (int u = 0; u < DA_U; ++u) {
+      const int key = k0 + 8 * u + ks;
+      if (key < hi) load8(vb + (int64_t)key * p.ldv, t[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < DA_U; ++u) {
+      const int key = k0 + 8 * u + ks;
+      if (key < hi) {
+        const float pe = F32 ? exp2f(sc[key - lo] - m) : __builtin_amdgcn_exp2f(sc[key - lo] - m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaf(pe, t[u][j], o[j]);
+        if (ch == 0) l += pe;
+      }
     }
   }
   // reduce over the 8 key slots of the wave (lanes ch, ch+8, ..., ch+56), then over waves
@@ -615,10 +633,16 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   p.v = v; p.ldv = ldv; p.svb = svb;
   p.o = o; p.sob = sob;
   p.H = H; p.Tk = Tk; p.tk_dev = tk_dev; p.c = scale * 1.4426950408889634f;
-  // fewer (clip, head) pairs than CUs over a long fixed key range (batch-1 long-form cross-attention):
-  // split the keys into chunks of DA_SPLIT over the grid's y dimension, then combine
-  const int nchunk = (Tk + DA_SPLIT - 1) / DA_SPLIT;
-  if (!tk_dev && B * H < 256 && nchunk >= 2) {
+  // few (clip, head) pairs (batch-1 long-form, small batches): split the keys into chunks of DA_SPLIT over
+  // the grid's y dimension, then combine.  Measured (tools/bench_decode_attn.py, H = 20, Tk = 1500): B = 1
+  // 26.9 -> 14.6 us, B = 16 46.9 -> 31.2 us; from B = 64 (1280 pairs) the one-workgroup-per-pair kernel is
+  // faster (90.6 vs 114.8 us).  With tk_dev (self-attention over a graph-captured cache) the host does
+  // not know Tk: the chunks cover the kernel's DA_MAX_TK bound and chunks past it store empty partials.
+  // TW_DECODE_SPLIT (A/B): 0 = never split, 2 = always, else (default) below 640 pairs.
+  static const int split_mode = [] { const char* e = getenv("TW_DECODE_SPLIT"); return e ? atoi(e) : 1; }();
+  const int nchunk = tk_dev ? DA_MAX_TK / DA_SPLIT : (Tk + DA_SPLIT - 1) / DA_SPLIT;
+  const bool split = split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
+  if (split && nchunk >= 2) {
     float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
     if (ws) {
       TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws);

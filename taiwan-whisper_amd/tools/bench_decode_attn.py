@@ -1,0 +1,35 @@
+"""tw_decode_attn A/B on the decode shapes: cross-attention over 1500 encoder frames (large-v2: H = 20)
+at batch 1 / 16 / 64 / 128; TW_DECODE_SPLIT selects the variant per process (0 never split, 1 default
+heuristic, 2 always split).  Prints us per call and the K/V read rate."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch
+
+from tw import ops
+
+
+def main():
+    H, Tk, d = 20, 1500, 1280
+    for B in (1, 16, 64, 128):
+        kv = torch.randn(B * Tk, 2 * d, device="cuda").bfloat16()
+        q = torch.randn(B, d, device="cuda").bfloat16()
+        o = torch.empty(B, d, dtype=torch.bfloat16, device="cuda")
+        run = lambda: ops.decode_attn(q, d, kv, 2 * d, Tk * 2 * d, kv[:, d:], 2 * d, Tk * 2 * d, o, d, B, H, Tk, 0.125)
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 50 * 1e3
+        print(f"split={os.environ.get('TW_DECODE_SPLIT', '1')} B={B:4d}: {us:8.1f} us  {B * Tk * 2 * d * 2 / us / 1e3:7.1f} GB/s",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

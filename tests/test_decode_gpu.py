@@ -1,8 +1,8 @@
 """Greedy KV-cache decoding on the GPU, bf16-autocast path.
 
 * tw_decode_attn vs an fp64 softmax-attention reference (single query row per (b, h), strided
-  caches; B*H < 256 over >= 2 chunks of keys runs the split-key variant + combine, B*H >= 256 the
-  one-workgroup-per-row kernel; Tk from 1 to 2048);
+  caches; B*H < 640 over >= 2 chunks of keys runs the split-key variant + combine, B*H >= 640 the
+  one-workgroup-per-row kernel; Tk from 1 to 2048, fixed or read from the device step counter);
 * tw_greedy_select vs torch (suppress / begin-suppress masks, ties -> lowest id, finished rows);
 * generate() KV cache vs a full recompute of the prefix with the same engine (every step);
 * generate() under bf16 autocast vs the bf16-autocast oracle (oracle/whisper_ref.Ref(amp=True), pinned to
@@ -33,9 +33,11 @@ def bf(x):
     return x.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("B,H,Tk", [(3, 2, 1), (2, 3, 5), (4, 20, 447), (2, 4, 1500), (1, 1, 2048), (1, 20, 1500),
-                                    (13, 20, 1500)])
-def test_decode_attn(B, H, Tk):
+@pytest.mark.parametrize("B,H,Tk,dev", [(3, 2, 1, False), (2, 3, 5, False), (4, 20, 447, False), (2, 4, 1500, False),
+                                        (1, 1, 2048, False), (1, 20, 1500, False), (13, 20, 1500, False),
+                                        (64, 20, 1500, False), (1, 20, 447, True), (40, 20, 200, True)])
+def test_decode_attn(B, H, Tk, dev):
+    """dev: Tk comes from the device step counter (graph-captured self-attention: Tk = 1 + *tk_dev)."""
     from tw import ops
     g = torch.Generator().manual_seed(B * 131 + Tk)
     d = H * 64
@@ -46,7 +48,12 @@ def test_decode_attn(B, H, Tk):
     flat = cd.view(-1)
     sb = Tmax * 3 * d
     o = torch.empty(B, d, dtype=torch.bfloat16, device=DEV)
-    ops.decode_attn(flat[t * 3 * d:], sb, flat[d:], 3 * d, sb, flat[2 * d:], 3 * d, sb, o, d, B, H, Tk, 0.125)
+    if dev:
+        t_dev = torch.tensor([Tk - 1], dtype=torch.int32, device=DEV)
+        ops.decode_attn(flat[t * 3 * d:], sb, flat[d:], 3 * d, sb, flat[2 * d:], 3 * d, sb, o, d, B, H, 1, 0.125,
+                        tk_dev=t_dev, tk_max=Tmax)
+    else:
+        ops.decode_attn(flat[t * 3 * d:], sb, flat[d:], 3 * d, sb, flat[2 * d:], 3 * d, sb, o, d, B, H, Tk, 0.125)
     q = cache[:, t, :d].double().view(B, H, 64)
     k = cache[:, :Tk, d:2 * d].double().view(B, Tk, H, 64).transpose(1, 2)
     v = cache[:, :Tk, 2 * d:].double().view(B, Tk, H, 64).transpose(1, 2)
