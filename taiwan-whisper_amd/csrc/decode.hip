@@ -637,11 +637,14 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   // the grid's y dimension, then combine.  Measured (tools/bench_decode_attn.py, H = 20, Tk = 1500): B = 1
   // 26.9 -> 14.6 us, B = 16 46.9 -> 31.2 us; from B = 64 (1280 pairs) the one-workgroup-per-pair kernel is
   // faster (90.6 vs 114.8 us).  With tk_dev (self-attention over a graph-captured cache) the host does
-  // not know Tk: the chunks cover the kernel's DA_MAX_TK bound and chunks past it store empty partials.
-  // TW_DECODE_SPLIT (A/B): 0 = never split, 2 = always, else (default) below 640 pairs.
+  // not know Tk, so the chunks would have to cover the kernel's DA_MAX_TK bound: measured on c5 (batch-1
+  // long-form, Tk <= 448) that costs more than it saves (2.75 -> 2.93 ms per decode step), so only
+  // TW_DECODE_SPLIT=3 (A/B) splits those.  TW_DECODE_SPLIT: 0 = never, 2 = every fixed-Tk call, else
+  // (default) fixed-Tk calls below 640 pairs.
   static const int split_mode = [] { const char* e = getenv("TW_DECODE_SPLIT"); return e ? atoi(e) : 1; }();
   const int nchunk = tk_dev ? DA_MAX_TK / DA_SPLIT : (Tk + DA_SPLIT - 1) / DA_SPLIT;
-  const bool split = split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
+  const bool split = tk_dev ? split_mode == 3 && B * H < 640
+                            : split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
   if (split && nchunk >= 2) {
     float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
     if (ws) {
