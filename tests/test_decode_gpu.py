@@ -36,7 +36,7 @@ def bf(x):
 @pytest.mark.parametrize("B,H,Tk,dev", [(3, 2, 1, False), (2, 3, 5, False), (4, 20, 447, False), (2, 4, 1500, False),
                                         (1, 1, 2048, False), (1, 20, 1500, False), (13, 20, 1500, False),
                                         (64, 20, 1500, False), (1, 20, 447, True), (40, 20, 200, True)])
-def test_decode_attn(B, H, Tk, dev, monkeypatch=None):
+def test_decode_attn(B, H, Tk, dev):
     """dev: Tk comes from the device step counter (graph-captured self-attention: Tk = 1 + *tk_dev)."""
     from tw import ops
     g = torch.Generator().manual_seed(B * 131 + Tk)
