@@ -24,17 +24,6 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const void* __
   }
 }
 
-__global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ dh, float* __restrict__ dE,
-                                 int rows, int D) {
-  const int row = blockIdx.x;
-  if (row >= rows) return;
-  const int64_t id = ids[row];
-  for (int e = threadIdx.x; e < D; e += blockDim.x) {
-    const float g = dh[(int64_t)row * D + e];
-    if (g != 0.f) atomicAdd(&dE[id * D + e], g);
-  }
-}
-
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int64_t n) {
   int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
@@ -246,13 +235,6 @@ extern "C" int tw_embed_fwd(const int64_t* ids, const void* tok, int tok_dtype, 
   if (rows <= 0) return TW_OK;
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(rows), dim3(256), 0, stream, ids, tok, tok_dtype, pos, pos_dtype, out,
                      out_dtype, rows, T, pos_offset, D);
-  TW_CHECK_LAUNCH();
-  return TW_OK;
-}
-
-extern "C" int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D, hipStream_t stream) {
-  if (rows <= 0) return TW_OK;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(rows), dim3(256), 0, stream, ids, dh, dE, rows, D);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
