@@ -50,6 +50,17 @@ int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t
                  float alpha, const void* bias, const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
                  void* aux, int64_t ldaux, int64_t sAux, int flags, tw_stream_t stream);
 
+/* Decode-step Linear for up to 4 rows (batch-1 long-form): C = epi(A . W^T), one output column per wave.
+ * A = x [M][K] bf16, or LayerNorm(x) when ln_w != NULL (fp32 gamma ln_w / beta ln_b, eps; K % 256 == 0;
+ * A is bit-identical to tw_layernorm_fwd's bf16 output, so an LN launch + GEMM pair becomes one launch).
+ * Replaces, per decode step, HF WhisperDecoderLayer's LayerNorm + nn.Linear pairs and the plain Linears
+ * (modeling_whisper.py:448-506) for a batch of <= 4.  W [N][K] bf16; flags / bias / res / aux as
+ * tw_gemm_bf16 (F_BIAS, F_ROUND, F_GELU, F_RES, F_AUX_OUT, F_ACCUM); C fp32 or bf16. */
+int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
+                 int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
+                 const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
+                 tw_stream_t stream);
+
 /* LayerNorm fp32-statistics forward / backward (D % 64 == 0, D <= 1280).
  * Replaces nn.LayerNorm at HF modeling_whisper.py:392,402,470,485,498,642,790 (autocast fp32 op). */
 int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, const float* b, void* y, int y_dtype,

@@ -491,6 +491,102 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmP p, int S) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// GEMV for the batch-1 (and up to 4-row) decode step: one output column per wave, 4 per workgroup
+// (N / 4 workgroups: 320 for N = 1280, where the 16-column skinny kernel has 80).  The A rows go to LDS
+// first -- as given, or through the LayerNorm in front of the Linear (ln_w != nullptr: the pre-LN residual
+// stream x in, the same half-wave statistics, order and bf16 output as ln_fwd_bf16_kernel, so A is
+// bit-identical to tw_layernorm_fwd's output) -- then each wave streams its W row (16 B per lane, up to
+// 4 loads in flight) against the LDS rows, fp32 FMAs in k order per lane, one butterfly sum, and lane 0
+// applies the full epilogue (epi_element).  Fusing the LN removes one launch per LN'd Linear, which is
+// most of a batch-1 step's cost (every launch there is latency-bound).
+// ---------------------------------------------------------------------------------------------
+template <int MR>
+__global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                   float eps) {
+  extern __shared__ __attribute__((aligned(16))) char gemv_smem[];
+  bf16* xs = (bf16*)gemv_smem;                         // [MR][K] bf16
+  const int lane = lane_id(), wave = wave_id_uniform();
+  const int K = p.K;
+  if (wave < MR) {
+    bf16* dst = xs + (int64_t)wave * K;
+    if (wave >= p.M) {
+      for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = bf16x8{};
+    } else if (lnw) {
+      const bf16* xr = p.A + (int64_t)wave * p.lda;
+      const int hl = lane & 31, nch = K / 256;
+      float s = 0.f;
+      for (int c = 0; c < nch; ++c) {
+        const bf16x8 t = *(const bf16x8*)(xr + (c * 32 + hl) * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += bf2f(t[q]);
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      const float mean = s / K;
+      float ss = 0.f;
+      for (int c = 0; c < nch; ++c) {
+        const bf16x8 t = *(const bf16x8*)(xr + (c * 32 + hl) * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { const float d = bf2f(t[q]) - mean; ss += d * d; }
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      const float rstd = rsqrtf(ss / K + eps);
+      if (lane < 32) {
+        for (int c = 0; c < nch; ++c) {
+          const int e = (c * 32 + hl) * 8;
+          const bf16x8 t = *(const bf16x8*)(xr + e);
+          const f32x4 w0 = *(const f32x4*)(lnw + e), w1 = *(const f32x4*)(lnw + e + 4);
+          const f32x4 b0 = *(const f32x4*)(lnb + e), b1 = *(const f32x4*)(lnb + e + 4);
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = bf2f(t[q]);
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            o[q] = f2bf((v[q] - mean) * rstd * w0[q] + b0[q]);
+            o[q + 4] = f2bf((v[q + 4] - mean) * rstd * w1[q] + b1[q]);
+          }
+          *(bf16x8*)(dst + e) = o;
+        }
+      }
+    } else {
+      const bf16* xr = p.A + (int64_t)wave * p.lda;
+      for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = *(const bf16x8*)(xr + e);
+    }
+  }
+  __syncthreads();
+  const int n = blockIdx.x * 4 + wave;
+  if (n >= p.N) return;
+  const bf16* wr = p.B + (int64_t)n * p.ldb;
+  float acc[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) acc[r] = 0.f;
+  for (int k0 = lane * 8; k0 < K; k0 += 4 * 512) {
+    bf16x8 w8[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w8[u] = (k0 + u * 512 < K) ? *(const bf16x8*)(wr + k0 + u * 512) : bf16x8{};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k0 + u * 512 < K) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+          const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + k0 + u * 512);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[r] = fmaf(bf2f(w8[u][q]), bf2f(a8[q]), acc[r]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < MR; ++r) acc[r] = wave_sum(acc[r]);
+  if (lane == 0)
+#pragma unroll
+    for (int r = 0; r < MR; ++r)
+      if (r < p.M) epi_element(p, r, n, acc[r]);
+}
+
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
   const dim3 grid((p.N + 15) / 16, S);
   const int mf = (p.M + 15) / 16;
@@ -743,6 +839,36 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   else if (!a_trans && b_trans) dispatch<false, true>(p, batch, stream, tile);
   else if (a_trans && !b_trans) dispatch<true, false>(p, batch, stream, tile);
   else dispatch<true, true>(p, batch, stream, tile);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
+                            int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
+                            const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
+                            hipStream_t stream) {
+  if (M <= 0 || N <= 0) return TW_OK;
+  if (M > 4 || K <= 0 || (K % 8) || (ldx % 8) || (ldw % 8)) return TW_EINVAL;
+  if (((uintptr_t)x & 15) || ((uintptr_t)W & 15)) return TW_EINVAL;
+  if (ln_w && (!ln_b || (K % 256) || (((uintptr_t)ln_w | (uintptr_t)ln_b) & 15))) return TW_EINVAL;
+  if ((flags & F_BIAS) && !bias) return TW_EINVAL;
+  if ((flags & F_RES) && !res) return TW_EINVAL;
+  if ((flags & (F_AUX_OUT | F_DGELU)) && !aux) return TW_EINVAL;
+  if (c_dtype != TW_F32 && c_dtype != TW_BF16) return TW_EUNSUPPORTED;
+  if ((size_t)4 * K * 2 > 64 * 1024) return TW_EUNSUPPORTED;        // A rows in LDS
+  GemmP p = {};
+  p.A = (const bf16*)x; p.B = (const bf16*)W; p.C = C;
+  p.lda = ldx; p.ldb = ldw; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+  p.alpha = 1.f; p.bias = (const bf16*)bias;
+  p.res = res; p.ldr = ldr; p.res_dtype = res_dtype; p.res_mod = 0;
+  p.aux = (bf16*)aux; p.ldaux = ldaux; p.c_dtype = c_dtype; p.flags = flags;
+  const dim3 grid((N + 3) / 4);
+  if (M == 1)
+    hipLaunchKernelGGL(gemv_kernel<1>, grid, dim3(256), (size_t)K * 2, stream, p, ln_w, ln_b, eps);
+  else if (M == 2)
+    hipLaunchKernelGGL(gemv_kernel<2>, grid, dim3(256), (size_t)2 * K * 2, stream, p, ln_w, ln_b, eps);
+  else
+    hipLaunchKernelGGL(gemv_kernel<4>, grid, dim3(256), (size_t)4 * K * 2, stream, p, ln_w, ln_b, eps);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -55,6 +55,11 @@ class DecodeSession:
         self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=act, device=dev)
         self.logits = torch.empty(B, model.Vp, dtype=act, device=dev)
         self.graph = None
+        # batch <= 4 on the bf16 path: every Linear is one tw_gemv_bf16 launch, with the LayerNorm in front
+        # of it fused when the residual stream is bf16 (bit-identical A); larger batches use the skinny
+        # GEMM with a separate LayerNorm
+        self.gemv = B <= 4 and model.compute == "bf16" and d % 256 == 0
+        self.gemv_ln = self.gemv and model.stream_dtype == torch.bfloat16
 
     def set_encoder(self, enc16):
         """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe)."""
@@ -70,6 +75,26 @@ class DecodeSession:
         F.layernorm_fwd(x, m.ln_param(name + ".weight"), m.ln_param(name + ".bias"), self.y)
         return self.y
 
+    def _ln_lin(self, x, ln, w, b, out, flags=F.GEMM_ROUND):
+        """out = Linear(LayerNorm(x)): one GEMV launch (batch <= 4, bf16 stream) or LN + GEMM."""
+        m = self.m
+        if self.gemv_ln:
+            F.gemv(x, w, out, ln_w=m.ln_param(ln + ".weight"), ln_b=m.ln_param(ln + ".bias"), bias=b, flags=flags)
+        else:
+            y = self._ln(x, ln)
+            if self.gemv:
+                F.gemv(y, w, out, bias=b, flags=flags)
+            else:
+                m._lin(y, w, b, out, flags=flags)
+        return out
+
+    def _lin(self, a, w, b, out, res=None, flags=F.GEMM_ROUND):
+        if self.gemv:
+            F.gemv(a, w, out, bias=b, res=res, flags=flags)
+        else:
+            self.m._lin(a, w, b, out, res=res, flags=flags)
+        return out
+
     def step(self, select=None):
         """One decoder step at position *t_dev for input ids `cur`; then t_dev += 1.
         select = (sup, beg, eos, done, ids, P) runs greedy selection into ids[:, t+1] and cur."""
@@ -84,29 +109,31 @@ class DecodeSession:
         for i in range(m.config.decoder_layers):
             p = f"model.decoder.layers.{i}"
             # self attention: fused QKV -> staging; k, v appended at row t of the cache
-            y = self._ln(x, p + ".self_attn_layer_norm")
             wqkv = m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d))
             bqkv = m.wspan(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,))
-            m._lin(y, wqkv, bqkv, self.qkv)
+            self._ln_lin(x, p + ".self_attn_layer_norm", wqkv, bqkv, self.qkv)
             cache = self.self_kv[i]
             F.kv_append(self.qkv[:, d:], 3 * d, cache, 2 * d, sb, B, 2 * d, t_dev, T_max)
             F.decode_attn(self.qkv, 3 * d, cache, 2 * d, sb, cache.view(-1)[d:], 2 * d, sb, o, d, B, H, 1, 0.125,
                           tk_dev=t_dev, tk_max=T_max)
-            m._lin(o, m._w16(p + ".self_attn.out_proj.weight"), m._w16(p + ".self_attn.out_proj.bias"), x, res=x)
+            self._lin(o, m._w16(p + ".self_attn.out_proj.weight"), m._w16(p + ".self_attn.out_proj.bias"), x, res=x)
             # cross attention over the encoder frames
-            y = self._ln(x, p + ".encoder_attn_layer_norm")
-            m._lin(y, m._w16(p + ".encoder_attn.q_proj.weight"), m._w16(p + ".encoder_attn.q_proj.bias"), self.q)
+            self._ln_lin(x, p + ".encoder_attn_layer_norm", m._w16(p + ".encoder_attn.q_proj.weight"),
+                         m._w16(p + ".encoder_attn.q_proj.bias"), self.q)
             kv = self.cross_kv[i]
             F.decode_attn(self.q, d, kv, 2 * d, self.Tk * 2 * d, kv[:, d:], 2 * d, self.Tk * 2 * d, o, d, B, H,
                           self.Tk, 0.125)
-            m._lin(o, m._w16(p + ".encoder_attn.out_proj.weight"), m._w16(p + ".encoder_attn.out_proj.bias"), x,
-                   res=x)
+            self._lin(o, m._w16(p + ".encoder_attn.out_proj.weight"), m._w16(p + ".encoder_attn.out_proj.bias"), x,
+                      res=x)
             # MLP
-            y = self._ln(x, p + ".final_layer_norm")
-            m._lin(y, m._w16(p + ".fc1.weight"), m._w16(p + ".fc1.bias"), self.h, flags=F.GEMM_ROUND | F.GEMM_GELU)
-            m._lin(self.h, m._w16(p + ".fc2.weight"), m._w16(p + ".fc2.bias"), x, res=x)
-        hN = self._ln(x, "model.decoder.layer_norm")
-        m.lm_head(hN, out=self.logits)
+            self._ln_lin(x, p + ".final_layer_norm", m._w16(p + ".fc1.weight"), m._w16(p + ".fc1.bias"), self.h,
+                         flags=F.GEMM_ROUND | F.GEMM_GELU)
+            self._lin(self.h, m._w16(p + ".fc2.weight"), m._w16(p + ".fc2.bias"), x, res=x)
+        if self.gemv_ln:
+            self._ln_lin(x, "model.decoder.layer_norm", m._w16("model.decoder.embed_tokens.weight"), None,
+                         self.logits)
+        else:
+            m.lm_head(self._ln(x, "model.decoder.layer_norm"), out=self.logits)
         if select is not None:
             select(self)
         F.step_advance(t_dev)

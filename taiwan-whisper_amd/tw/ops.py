@@ -83,6 +83,32 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     return C
 
 
+def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=None, flags=0):
+    """tw_gemv_bf16: C[m] = epi(A[m] . W^T) for M <= 4 rows, A = x or LayerNorm(x) (ln_w / ln_b given):
+    the batch-1 decode step's LN + Linear pairs in one launch (include/tw_hip.h)."""
+    M, K = x.shape
+    N = W.shape[0]
+    assert x.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and M <= 4 and W.shape[1] == K
+    assert x.stride(1) == 1 and W.is_contiguous()
+    _need(C, (M - 1) * C.stride(0) + N, "gemv C")
+    if ln_w is not None:
+        assert ln_w.dtype == torch.float32 and ln_b.dtype == torch.float32 and ln_w.numel() == K == ln_b.numel()
+    if bias is not None:
+        assert bias.dtype == torch.bfloat16 and bias.numel() >= N
+        flags |= GEMM_BIAS
+    if res is not None:
+        _need(res, (M - 1) * res.stride(0) + N, "gemv residual")
+        flags |= GEMM_RES
+    if aux is not None:
+        assert aux.dtype == torch.bfloat16
+        _need(aux, (M - 1) * aux.stride(0) + N, "gemv aux")
+    KernelTimer.wrap("gemv", 2.0 * M * N * K, lambda: call(
+        "tw_gemv_bf16", x.data_ptr(), x.stride(0), _ptr(ln_w), _ptr(ln_b), float(eps), W.data_ptr(), K, C.data_ptr(),
+        C.stride(0), _dt(C), M, N, K, _ptr(bias), _ptr(res), res.stride(0) if res is not None else 0,
+        _dt(res) if res is not None else F32, _ptr(aux), aux.stride(0) if aux is not None else 0, flags, _stream()))
+    return C
+
+
 def layernorm_fwd(x, w, b, y, mean=None, rstd=None, eps=1e-5):
     D = x.shape[-1]
     rows = x.numel() // D

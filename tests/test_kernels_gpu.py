@@ -548,6 +548,52 @@ def test_logmel_longform_matches_oracle_and_hf():
     assert torch.equal(a, b)
 
 
+# ----------------------------------------------------------------------------- decode GEMV
+@pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (2, 3840, 1280), (4, 1280, 5120), (3, 520, 256), (1, 51904, 1280)])
+def test_gemv_decode(M, N, K):
+    """tw_gemv_bf16 (batch <= 4 decode Linears) vs an fp64 reference of the bf16 operands (fp32 accumulation
+    in another order: within one bf16 ulp of the rounded output + 1e-5 abs); the fused LayerNorm is
+    bit-identical to tw_layernorm_fwd's bf16 output (same GEMV over the unfused A: identical bits); every
+    epilogue the decode step uses (bias + round, + GELU with the pre-activation, + bf16 / fp32 residual)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    x = bf(torch.randn(M, K, generator=g) * 2 + 0.5)
+    W = bf(torch.randn(N, K, generator=g) * 0.03)
+    b = bf(torch.randn(N, generator=g) * 0.1)
+    lw, lb = torch.randn(K, generator=g) * 0.2 + 1, torch.randn(K, generator=g) * 0.1
+    xd, Wd, bd, lwd, lbd = x.to(DEV), W.to(DEV), b.to(DEV), lw.to(DEV), lb.to(DEV)
+    # plain: C = round(A W^T + b)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemv(xd, Wd, C, bias=bd, flags=ops.GEMM_ROUND)
+    ref = x.double() @ W.double().t() + b.double()
+    err = (C.double().cpu() - ref).abs()
+    assert (err <= 2 ** -8 * ref.abs() + 1e-5).all(), float(err.max())
+    # fused LayerNorm == LayerNorm kernel then GEMV, bit for bit
+    y = torch.empty_like(xd)
+    ops.layernorm_fwd(xd, lwd, lbd, y)
+    C1 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    C2 = torch.empty_like(C1)
+    ops.gemv(xd, Wd, C1, ln_w=lwd, ln_b=lbd, bias=bd, flags=ops.GEMM_ROUND)
+    ops.gemv(y, Wd, C2, bias=bd, flags=ops.GEMM_ROUND)
+    assert torch.equal(C1, C2)
+    # GELU with the pre-activation output
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    pre = torch.empty_like(h)
+    ops.gemv(y, Wd, h, bias=bd, aux=pre, flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT)
+    assert torch.equal(pre, C2)
+    gl = torch.nn.functional.gelu(pre.float()).to(torch.bfloat16)
+    assert ((h.float() - gl.float()).abs() <= 2 ** -8 * gl.float().abs() + 1e-6).all()
+    # residual, in place, bf16 and fp32 streams
+    for dt in (torch.bfloat16, torch.float32):
+        if N != K:
+            continue
+        r = (torch.randn(M, N, generator=g)).to(dt).to(DEV)
+        r0 = r.clone()
+        ops.gemv(y, Wd, r, bias=bd, res=r, flags=ops.GEMM_ROUND)
+        want = C2.float() + r0.float()
+        assert ((r.float() - want).abs() <= (2 ** -8 * want.abs() if dt == torch.bfloat16 else 1e-6)).all()
+
+
 # ----------------------------------------------------------------------------- misc
 def test_embed_adamw_norm_shift():
     from tw import ops
