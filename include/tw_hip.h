@@ -217,6 +217,14 @@ int tw_im2col3_f32(const float* src, int64_t src_rows, float* dst, int B, int T_
                    tw_stream_t stream);
 int tw_gelu_bwd_f32(const float* g, const float* pre, float* out, int64_t n, tw_stream_t stream);
 
+/* ---- host code: FLAC decoding for the data feed (replaces soundfile / libsndfile's sf.read of the
+ * reference corpus, dataset/cool_dataset.py:55).  `data` is the whole file in host memory.
+ * tw_flac_info: info[4] = {channels, sample_rate, bits_per_sample, total samples per channel (0 = unknown)}.
+ * tw_flac_decode: interleaved int32 samples into out[cap] (out == NULL: count only), *frames = samples per
+ * channel; every frame's CRC-8 header and CRC-16 footer is checked (1 = malformed stream). */
+int tw_flac_info(const uint8_t* data, int64_t n, int64_t* info);
+int tw_flac_decode(const uint8_t* data, int64_t n, int32_t* out, int64_t cap, int64_t* frames);
+
 #ifdef __cplusplus
 }
 #endif

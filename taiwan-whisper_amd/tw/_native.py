@@ -18,6 +18,8 @@ P, I64, I32, F32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "tw_gemm_bf16": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I32, I64, I64, I64, F32, P,
                      P, I64, I64, I32, I32, P, I64, I64, I32, P],
+    "tw_flac_info": [P, I64, P],
+    "tw_flac_decode": [P, I64, P, I64, P],
     "tw_gemv_bf16": [P, I64, P, P, F32, P, I64, P, I64, I32, I32, I32, I32, P, P, I64, I32, P, I64, I32, P],
     "tw_layernorm_fwd": [P, I32, P, P, P, I32, P, P, I32, I32, F32, P],
     "tw_layernorm_bwd": [P, I32, P, P, P, P, I32, P, I32, P, P, I32, I32, P, I64, P],

@@ -23,9 +23,10 @@ Differences by design: each rank reads only its own clips (no rank-0 read + broa
 step); log-mel runs on the GPU (tw_logmel) instead of CPU dataloader workers; host work
 (audio decode, tokenization, label sampling) runs in a thread pool ahead of the step.
 
-Audio decoding: soundfile (libsndfile, FLAC) when importable, as the reference; without it (this
-image) WAV (PCM 8/16/24/32-bit, float32) via the standard library and .npy arrays are read natively,
-and FLAC raises with a message naming the missing dependency.
+Audio decoding: soundfile (libsndfile) when importable, as the reference; without it (this image) FLAC
+through the native decoder in libtw_hip.so (tw_flac_decode, host code: csrc/flac.cpp), WAV (PCM
+8/16/24/32-bit) via the standard library and .npy arrays; samples as soundfile returns them (float64,
+integer PCM / 2^(bits-1)).
 """
 from __future__ import annotations
 
@@ -62,6 +63,23 @@ def load_audio_fpaths(manifest_fpath: str, root: Optional[str] = None) -> List[s
     return out
 
 
+def decode_flac(data: bytes):
+    """FLAC bytes -> (float64 samples [n] or [n, channels] scaled like soundfile.read, sample rate), via
+    tw_flac_info / tw_flac_decode (frame CRCs checked; a malformed stream raises)."""
+    import ctypes
+    from ._native import call
+    buf = np.frombuffer(data, dtype=np.uint8)
+    info = np.zeros(4, dtype=np.int64)
+    call("tw_flac_info", buf.ctypes.data, buf.size, info.ctypes.data)
+    ch, sr, bps = int(info[0]), int(info[1]), int(info[2])
+    frames = ctypes.c_int64(0)
+    call("tw_flac_decode", buf.ctypes.data, buf.size, None, 0, ctypes.addressof(frames))
+    out = np.empty(frames.value * ch, dtype=np.int32)
+    call("tw_flac_decode", buf.ctypes.data, buf.size, out.ctypes.data, out.size, ctypes.addressof(frames))
+    x = out.astype(np.float64) / float(1 << (bps - 1))
+    return (x.reshape(-1, ch) if ch > 1 else x), sr
+
+
 def read_audio(path: str):
     """-> (float64 samples in [-1, 1), sampling rate), like soundfile.read(path)."""
     try:
@@ -71,6 +89,9 @@ def read_audio(path: str):
     except ImportError:
         pass
     ext = osp.splitext(path)[1].lower()
+    if ext == ".flac":
+        with open(path, "rb") as f:
+            return decode_flac(f.read())
     if ext == ".npy":
         return np.load(path).astype(np.float64), SAMPLING_RATE
     if ext == ".wav":
