@@ -568,21 +568,27 @@ def test_gemv_decode(M, N, K):
     ref = x.double() @ W.double().t() + b.double()
     err = (C.double().cpu() - ref).abs()
     assert (err <= 2 ** -8 * ref.abs() + 1e-5).all(), float(err.max())
-    # fused LayerNorm == LayerNorm kernel then GEMV, bit for bit
+    # fused LayerNorm == LayerNorm kernel then GEMV, bit for bit (the LN kernel takes rows up to 1280;
+    # the decode step's LN'd Linears all have K = d_model)
     y = torch.empty_like(xd)
-    ops.layernorm_fwd(xd, lwd, lbd, y)
-    C1 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    C2 = torch.empty_like(C1)
-    ops.gemv(xd, Wd, C1, ln_w=lwd, ln_b=lbd, bias=bd, flags=ops.GEMM_ROUND)
-    ops.gemv(y, Wd, C2, bias=bd, flags=ops.GEMM_ROUND)
-    assert torch.equal(C1, C2)
+    C2 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    if K <= 1280:
+        ops.layernorm_fwd(xd, lwd, lbd, y)
+        C1 = torch.empty_like(C2)
+        ops.gemv(xd, Wd, C1, ln_w=lwd, ln_b=lbd, bias=bd, flags=ops.GEMM_ROUND)
+        ops.gemv(y, Wd, C2, bias=bd, flags=ops.GEMM_ROUND)
+        assert torch.equal(C1, C2)
+    else:
+        y.copy_(xd)
+        ops.gemv(y, Wd, C2, bias=bd, flags=ops.GEMM_ROUND)
     # GELU with the pre-activation output
     h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     pre = torch.empty_like(h)
     ops.gemv(y, Wd, h, bias=bd, aux=pre, flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT)
     assert torch.equal(pre, C2)
-    gl = torch.nn.functional.gelu(pre.float()).to(torch.bfloat16)
-    assert ((h.float() - gl.float()).abs() <= 2 ** -8 * gl.float().abs() + 1e-6).all()
+    # the epilogue's erf GELU vs PyTorch's fp32 formula: 1 bf16 ulp or 5e-7 (test_gemm_gelu_exhaustive)
+    gl = torch.nn.functional.gelu(pre.float())
+    assert ((h.float() - gl).abs() <= torch.maximum(gl.abs() * 2 ** -7, torch.full_like(gl, 5e-7))).all()
     # residual, in place, bf16 and fp32 streams
     for dt in (torch.bfloat16, torch.float32):
         if N != K:
