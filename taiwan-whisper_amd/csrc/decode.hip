@@ -177,21 +177,32 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, i
   decode_attn_body<E>(p, b, h, lo, hi, part);
 }
 
-// O = sum_c 2^(m_c - M) o_c / sum_c 2^(m_c - M) l_c over the chunks of one (clip, head), in chunk order
+// O = sum_c 2^(m_c - M) o_c / sum_c 2^(m_c - M) l_c over the chunks of one (clip, head), in chunk order.
+// Lane c loads chunk c's (m, l) and every lane its column of all chunks up front (nchunk <= DA_MAX_CHUNK
+// independent loads in flight instead of a dependent chain), weights broadcast by shuffles.
+constexpr int DA_MAX_CHUNK = 16;
 template <typename E>
 __global__ __launch_bounds__(64) void decode_attn_combine_kernel(DecP p, int nchunk, const float* ws) {
   const int bh = blockIdx.x, tid = threadIdx.x;
   const int b = bh / p.H, h = bh % p.H;
   const float* part = ws + (int64_t)bh * nchunk * 66;
-  float M = -INFINITY;
-  for (int c = 0; c < nchunk; ++c) M = fmaxf(M, part[c * 66 + 64]);
+  const float mc = tid < nchunk ? part[tid * 66 + 64] : -INFINITY;
+  const float lc = tid < nchunk ? part[tid * 66 + 65] : 0.f;
+  float oc[DA_MAX_CHUNK];
+#pragma unroll
+  for (int c = 0; c < DA_MAX_CHUNK; ++c) oc[c] = c < nchunk ? part[c * 66 + tid] : 0.f;
+  const float M = wave_max(mc);
+  const float wc = mc == -INFINITY ? 0.f : (sizeof(E) == 4 ? exp2f(mc - M) : __builtin_amdgcn_exp2f(mc - M));
   float acc = 0.f, lt = 0.f;
-  for (int c = 0; c < nchunk; ++c) {
-    const float mc = part[c * 66 + 64];
-    if (mc == -INFINITY) continue;
-    const float w = sizeof(E) == 4 ? exp2f(mc - M) : __builtin_amdgcn_exp2f(mc - M);
-    acc = fmaf(w, part[c * 66 + tid], acc);
-    lt = fmaf(w, part[c * 66 + 65], lt);
+#pragma unroll
+  for (int c = 0; c < DA_MAX_CHUNK; ++c) {
+    if (c < nchunk) {
+      const float w = __shfl(wc, c, 64), l = __shfl(lc, c, 64);
+      if (__shfl(mc, c, 64) != -INFINITY) {
+        acc = fmaf(w, oc[c], acc);
+        lt = fmaf(w, l, lt);
+      }
+    }
   }
   from_f32(((E*)p.o)[b * p.sob + h * 64 + tid], acc / lt);
 }
@@ -216,8 +227,9 @@ struct SelP {
 // f(v, x, suppressed, begin_suppressed) over this thread's ids of a logits row: chunks of 8
 // consecutive ids (one 16-B load, one word of each mask), chunk c = tid, tid + 256, ...
 template <typename E, class F>
-__device__ __forceinline__ void for_row(const SelP& p, const E* row, F&& f) {
-  for (int v0 = (int)threadIdx.x * 8; v0 < p.V; v0 += 256 * 8) {
+__device__ __forceinline__ void for_row(const SelP& p, const E* row, F&& f, int lo = 0, int hi = -1) {
+  if (hi < 0) hi = p.V;                                  // [lo, hi), lo a multiple of 8
+  for (int v0 = lo + (int)threadIdx.x * 8; v0 < hi; v0 += 256 * 8) {
     float xs[8];
     if (p.vec) {
       load8(row + v0, xs);
@@ -229,7 +241,7 @@ __device__ __forceinline__ void for_row(const SelP& p, const E* row, F&& f) {
     const uint32_t wb = p.begin ? p.begin[v0 >> 5] >> (v0 & 31) : 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (v0 + j < p.V) f(v0 + j, xs[j], ((ws >> j) & 1u) != 0u, ((wb >> j) & 1u) != 0u);
+      if (v0 + j < hi) f(v0 + j, xs[j], ((ws >> j) & 1u) != 0u, ((wb >> j) & 1u) != 0u);
   }
 }
 
@@ -289,46 +301,113 @@ __device__ __forceinline__ void block_lse(float& m, float& s, float (*sv)[4], in
 
 __device__ __forceinline__ bool bit(const uint32_t* m, int v) { return m && ((m[v >> 5] >> (v & 31)) & 1u); }
 
+// Selection over a row is split into scan (per-thread accumulation over a slice of the vocabulary),
+// block reduction, and finish (thread 0: merge, pick, bookkeeping).  Few rows (batch-1 long-form): the
+// row is cut into G slices, one workgroup each, partials to the per-device scratch block, and a second
+// kernel merges them in slice order and finishes -- one 256-thread workgroup per row scanning 51 865
+// logits took ~78 us per step; many rows: one workgroup per row does all three.
+struct GreedyAcc {
+  float best, sbest, m, se;
+  int besti, sbesti;
+};
+constexpr int SEL_WORDS = 8;     // words per partial in the scratch block
+
+__device__ __forceinline__ void greedy_init(GreedyAcc& a) {
+  a.best = a.sbest = a.m = -INFINITY;
+  a.se = 0.f;
+  a.besti = a.sbesti = 0x7fffffff;
+}
+__device__ __forceinline__ void greedy_merge(GreedyAcc& a, const GreedyAcc& o, bool sample, bool lse) {
+  if (o.best > a.best || (o.best == a.best && o.besti < a.besti)) { a.best = o.best; a.besti = o.besti; }
+  if (sample && (o.sbest > a.sbest || (o.sbest == a.sbest && o.sbesti < a.sbesti))) { a.sbest = o.sbest; a.sbesti = o.sbesti; }
+  if (lse) lse_merge(a.m, a.se, o.m, o.se);
+}
 template <typename E>
-__global__ __launch_bounds__(256) void greedy_select_kernel(SelP p) {
-  __shared__ float sv[4][4];
-  __shared__ int si[4][4];
-  const int b = blockIdx.x, tid = threadIdx.x;
+__device__ __forceinline__ void greedy_scan(const SelP& p, const E* row, int b, bool sample, float inv_t, uint64_t seed,
+                                            GreedyAcc& a, int lo, int hi) {
+  const bool lse = p.sum_logp != nullptr;
+  for_row(p, row, [&](int v, float x, bool sup, bool beg) {
+    if (sup || (p.apply_begin && beg)) x = -INFINITY;
+    if (x > a.best || (x == a.best && v < a.besti)) { a.best = x; a.besti = v; }
+    if (x > -INFINITY) {
+      if (lse) lse_add(a.m, a.se, x);
+      if (sample) {
+        const float g = x * inv_t + gumbel(seed, b, p.col, v);
+        if (g > a.sbest || (g == a.sbest && v < a.sbesti)) { a.sbest = g; a.sbesti = v; }
+      }
+    }
+  }, lo, hi);
+}
+// block reduction: the result in thread 0's a
+__device__ __forceinline__ void greedy_block(GreedyAcc& a, bool sample, bool lse, float (*sv)[4], int (*si)[4]) {
+  block_argmax(a.best, a.besti, sv, si, 0);
+  if (sample) block_argmax(a.sbest, a.sbesti, sv, si, 1);
+  if (lse) block_lse(a.m, a.se, sv, 2);
+}
+template <typename E>
+__device__ __forceinline__ void greedy_finish(const SelP& p, const E* row, int b, const GreedyAcc& a, bool sample) {
+  int pick = sample ? a.sbesti : a.besti;
+  if (pick == 0x7fffffff) pick = 0;              // every logit masked / NaN: id 0 (torch argmax of all -inf)
+  const bool fin = p.done[b] != 0;
+  const int64_t tok = fin ? p.eos : (int64_t)pick;
+  p.ids[b * p.ld_ids + p.col] = tok;
+  p.next[b] = tok;
+  p.done[b] = (fin || tok == p.eos) ? 1 : 0;
+  if (p.sum_logp && !fin) p.sum_logp[b] += to_f32(row[pick]) - lse_val(a.m, a.se);
+}
+__device__ __forceinline__ void sel_prologue(SelP& p) {
   if (p.t_dev) {
     p.col += *p.t_dev;
     p.apply_begin = p.col == p.begin_col;
   }
+}
+
+// grid (G, B): G == 1 -> scan the whole row and finish; G > 1 -> partial of slice blockIdx.x into ws
+template <typename E>
+__global__ __launch_bounds__(256) void greedy_select_kernel(SelP p, int slice, float* ws) {
+  __shared__ float sv[4][4];
+  __shared__ int si[4][4];
+  const int g = blockIdx.x, G = gridDim.x, b = blockIdx.y, tid = threadIdx.x;
+  sel_prologue(p);
   float inv_t;
   uint64_t seed;
   read_ctl(p.ctl, inv_t, seed);
-  const bool sample = inv_t > 0.f;
+  const bool sample = inv_t > 0.f, lse = p.sum_logp != nullptr;
   const E* row = (const E*)p.logits + b * p.ld;
-  float best = -INFINITY, sbest = -INFINITY, m = -INFINITY, se = 0.f;
-  int besti = 0x7fffffff, sbesti = 0x7fffffff;
-  for_row(p, row, [&](int v, float x, bool sup, bool beg) {
-    if (sup || (p.apply_begin && beg)) x = -INFINITY;
-    if (x > best || (x == best && v < besti)) { best = x; besti = v; }
-    if (x > -INFINITY) {
-      lse_add(m, se, x);
-      if (sample) {
-        const float g = x * inv_t + gumbel(seed, b, p.col, v);
-        if (g > sbest || (g == sbest && v < sbesti)) { sbest = g; sbesti = v; }
-      }
-    }
-  });
-  block_argmax(best, besti, sv, si, 0);
-  if (sample) block_argmax(sbest, sbesti, sv, si, 1);
-  if (p.sum_logp) block_lse(m, se, sv, 2);
-  if (tid == 0) {
-    int pick = sample ? sbesti : besti;
-    if (pick == 0x7fffffff) pick = 0;              // every logit masked / NaN: id 0 (torch argmax of all -inf)
-    const bool fin = p.done[b] != 0;
-    const int64_t tok = fin ? p.eos : (int64_t)pick;
-    p.ids[b * p.ld_ids + p.col] = tok;
-    p.next[b] = tok;
-    p.done[b] = (fin || tok == p.eos) ? 1 : 0;
-    if (p.sum_logp && !fin) p.sum_logp[b] += to_f32(row[pick]) - lse_val(m, se);
+  GreedyAcc a;
+  greedy_init(a);
+  const int lo = G == 1 ? 0 : g * slice, hi = G == 1 ? p.V : min(p.V, lo + slice);
+  greedy_scan(p, row, b, sample, inv_t, seed, a, lo, hi);
+  greedy_block(a, sample, lse, sv, si);
+  if (tid != 0) return;
+  if (G == 1) {
+    greedy_finish(p, row, b, a, sample);
+  } else {
+    float* w = ws + ((int64_t)b * G + g) * SEL_WORDS;
+    w[0] = a.best; w[1] = a.sbest; w[2] = a.m; w[3] = a.se;
+    w[4] = __int_as_float(a.besti); w[5] = __int_as_float(a.sbesti);
   }
+}
+
+template <typename E>
+__global__ __launch_bounds__(64) void greedy_merge_kernel(SelP p, int G, const float* ws) {
+  const int b = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  sel_prologue(p);
+  float inv_t;
+  uint64_t seed;
+  read_ctl(p.ctl, inv_t, seed);
+  const bool sample = inv_t > 0.f, lse = p.sum_logp != nullptr;
+  GreedyAcc a;
+  greedy_init(a);
+  for (int g = 0; g < G; ++g) {
+    const float* w = ws + ((int64_t)b * G + g) * SEL_WORDS;
+    GreedyAcc o;
+    o.best = w[0]; o.sbest = w[1]; o.m = w[2]; o.se = w[3];
+    o.besti = __float_as_int(w[4]); o.sbesti = __float_as_int(w[5]);
+    greedy_merge(a, o, sample, lse);
+  }
+  greedy_finish(p, (const E*)p.logits + b * p.ld, b, a, sample);
 }
 
 
@@ -347,89 +426,107 @@ struct SelTsP {
   int* last_ts;
 };
 
+struct TsAcc {
+  float bt, bs, se, tm, tse;      // best text, best timestamp, sum exp(ts - bs), text logsumexp (m, s)
+  int it, is;
+};
+__device__ __forceinline__ void ts_init(TsAcc& a) {
+  a.bt = a.bs = a.tm = -INFINITY;
+  a.se = a.tse = 0.f;
+  a.it = a.is = 0x7fffffff;
+}
+__device__ __forceinline__ void ts_merge(TsAcc& a, const TsAcc& o, bool lse) {
+  if (o.bt > a.bt || (o.bt == a.bt && o.it < a.it)) { a.bt = o.bt; a.it = o.it; }
+  const float mx = fmaxf(a.bs, o.bs);
+  const float ns = (mx == -INFINITY) ? 0.f : a.se * __expf(a.bs - mx) + o.se * __expf(o.bs - mx);
+  if (o.bs > a.bs || (o.bs == a.bs && o.is < a.is)) a.is = o.is;
+  a.bs = mx;
+  a.se = ns;
+  if (lse) lse_merge(a.tm, a.tse, o.tm, o.tse);
+}
+// the row's timestamp-rule state at column p.col
+struct TsRow {
+  bool first, last_ts, pen_ts;
+  int lim, ts_hi;
+};
+__device__ __forceinline__ TsRow ts_row(const SelTsP& q, int b) {
+  const SelP& p = q.s;
+  TsRow r;
+  r.first = p.col == q.begin_col;
+  const int64_t* idr = p.ids + b * p.ld_ids;
+  const bool has1 = p.col - 1 >= q.begin_col, has2 = p.col - 2 >= q.begin_col;
+  r.last_ts = has1 && idr[p.col - 1] >= q.ts_begin;
+  r.pen_ts = !has2 || idr[p.col - 2] >= q.ts_begin;
+  const int lt = q.last_ts[b];
+  r.lim = lt < 0 ? q.ts_begin : ((r.last_ts && !r.pen_ts) ? lt : lt + 1);
+  r.ts_hi = (r.first && q.max_initial >= 0) ? q.ts_begin + q.max_initial : 0x7fffffff;
+  return r;
+}
+// eligibility of id v before the "timestamp mass wins" rule
+__device__ __forceinline__ bool ts_masked(const SelTsP& q, const TsRow& r, int v, bool sup, bool beg) {
+  bool m = sup || (r.first && beg) || v == q.no_ts;
+  if (v >= q.ts_begin) {
+    if (r.last_ts && r.pen_ts) m = true;
+    if (v < r.lim || v > r.ts_hi) m = true;
+  } else if ((r.last_ts && !r.pen_ts && v < q.s.eos) || r.first) {
+    m = true;
+  }
+  return m;
+}
 template <typename E>
-__global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
-  __shared__ float sv[4][3];
-  __shared__ int si[4][2];
-  __shared__ float sx[4][4];
-  __shared__ int sxi[4][4];
-  __shared__ float s_tm, s_ts, s_bt, s_bs;
+__device__ __forceinline__ void ts_scan(const SelTsP& q, const TsRow& r, const E* row, TsAcc& a, int lo, int hi) {
+  const bool lse = q.s.sum_logp != nullptr;
+  for_row(q.s, row, [&](int v, float x, bool sup, bool beg) {
+    if (ts_masked(q, r, v, sup, beg) || !(x > -INFINITY)) return;
+    if (v >= q.ts_begin) {
+      if (x > a.bs) { a.se = a.se * __expf(a.bs - x) + 1.f; a.bs = x; a.is = v; }
+      else { a.se += __expf(x - a.bs); if (x == a.bs && v < a.is) a.is = v; }
+    } else {
+      if (x > a.bt || (x == a.bt && v < a.it)) { a.bt = x; a.it = v; }
+      if (lse) lse_add(a.tm, a.tse, x);
+    }
+  }, lo, hi);
+}
+// block reduction (waves by shuffles, then thread 0 over the 4 waves): the result in thread 0's a
+__device__ __forceinline__ void ts_block(TsAcc& a, bool lse, float (*sv)[8], int (*si)[2]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    TsAcc x;
+    x.bt = __shfl_xor(a.bt, o, 64); x.bs = __shfl_xor(a.bs, o, 64); x.se = __shfl_xor(a.se, o, 64);
+    x.tm = __shfl_xor(a.tm, o, 64); x.tse = __shfl_xor(a.tse, o, 64);
+    x.it = __shfl_xor(a.it, o, 64); x.is = __shfl_xor(a.is, o, 64);
+    ts_merge(a, x, lse);
+  }
+  if (lane == 0) {
+    sv[wave][0] = a.bt; sv[wave][1] = a.bs; sv[wave][2] = a.se; sv[wave][3] = a.tm; sv[wave][4] = a.tse;
+    si[wave][0] = a.it; si[wave][1] = a.is;
+  }
+  __syncthreads();
+  if (tid == 0)
+    for (int w = 1; w < 4; ++w) {
+      TsAcc x;
+      x.bt = sv[w][0]; x.bs = sv[w][1]; x.se = sv[w][2]; x.tm = sv[w][3]; x.tse = sv[w][4];
+      x.it = si[w][0]; x.is = si[w][1];
+      ts_merge(a, x, lse);
+    }
+}
+// finish (whole workgroup; the merged accumulator in thread 0's a): the timestamp-mass rule, the
+// temperature-sampling pass over the processed row (Gumbel-max) when T > 0, the pick and bookkeeping
+template <typename E>
+__device__ __forceinline__ void ts_finish(const SelTsP& q, const TsRow& r, int b, TsAcc& a, float (*sx)[4],
+                                          int (*sxi)[4]) {
   __shared__ int s_mask_text;
-  SelP& p = q.s;
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (p.t_dev) p.col += *p.t_dev;
+  const SelP& p = q.s;
+  const int tid = threadIdx.x;
   float inv_t;
   uint64_t seed;
   read_ctl(p.ctl, inv_t, seed);
   const bool sample = inv_t > 0.f;
-  const bool first = p.col == q.begin_col;
-  const int64_t* idr = p.ids + b * p.ld_ids;
-  const bool has1 = p.col - 1 >= q.begin_col, has2 = p.col - 2 >= q.begin_col;
-  const bool last_ts = has1 && idr[p.col - 1] >= q.ts_begin;
-  const bool pen_ts = !has2 || idr[p.col - 2] >= q.ts_begin;
-  const int lt = q.last_ts[b];
-  const int lim = lt < 0 ? q.ts_begin : ((last_ts && !pen_ts) ? lt : lt + 1);
-  const int ts_hi = (first && q.max_initial >= 0) ? q.ts_begin + q.max_initial : 0x7fffffff;
   const E* row = (const E*)p.logits + b * p.ld;
-  // eligibility of id v before the "timestamp mass wins" rule
-  auto masked = [&](int v, bool sup, bool beg) -> bool {
-    bool m = sup || (first && beg) || v == q.no_ts;
-    if (v >= q.ts_begin) {
-      if (last_ts && pen_ts) m = true;
-      if (v < lim || v > ts_hi) m = true;
-    } else if ((last_ts && !pen_ts && v < p.eos) || first) {
-      m = true;
-    }
-    return m;
-  };
-  float bt = -INFINITY, bs = -INFINITY, se = 0.f;        // best text, best timestamp, sum exp(ts - bs)
-  float tm = -INFINITY, tse = 0.f;                       // text logsumexp (for the log-prob)
-  int it = 0x7fffffff, is = 0x7fffffff;
-  for_row(p, row, [&](int v, float x, bool sup, bool beg) {
-    if (masked(v, sup, beg) || !(x > -INFINITY)) return;
-    if (v >= q.ts_begin) {
-      if (x > bs) { se = se * __expf(bs - x) + 1.f; bs = x; is = v; }
-      else { se += __expf(x - bs); if (x == bs && v < is) is = v; }
-    } else {
-      if (x > bt || (x == bt && v < it)) { bt = x; it = v; }
-      lse_add(tm, tse, x);
-    }
-  });
-  // wave reduction: text (max, argmin idx), timestamps (max, argmin idx, rescaled sum)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float obt = __shfl_xor(bt, o, 64), obs = __shfl_xor(bs, o, 64), ose = __shfl_xor(se, o, 64);
-    const int oit = __shfl_xor(it, o, 64), ois = __shfl_xor(is, o, 64);
-    if (obt > bt || (obt == bt && oit < it)) { bt = obt; it = oit; }
-    const float mx = fmaxf(bs, obs);
-    const float ns = (mx == -INFINITY) ? 0.f : se * __expf(bs - mx) + ose * __expf(obs - mx);
-    if (obs > bs || (obs == bs && ois < is)) is = ois;
-    bs = mx;
-    se = ns;
-    lse_merge(tm, tse, __shfl_xor(tm, o, 64), __shfl_xor(tse, o, 64));
-  }
-  if (lane == 0) {
-    sv[wave][0] = bt; sv[wave][1] = bs; sv[wave][2] = se; si[wave][0] = it; si[wave][1] = is;
-    sx[0][wave] = tm; sx[1][wave] = tse;
-  }
-  __syncthreads();
   if (tid == 0) {
-    for (int w = 1; w < 4; ++w) {
-      const float obt = sv[w][0], obs = sv[w][1], ose = sv[w][2];
-      const int oit = si[w][0], ois = si[w][1];
-      if (obt > bt || (obt == bt && oit < it)) { bt = obt; it = oit; }
-      const float mx = fmaxf(bs, obs);
-      const float ns = (mx == -INFINITY) ? 0.f : se * __expf(bs - mx) + ose * __expf(obs - mx);
-      if (obs > bs || (obs == bs && ois < is)) is = ois;
-      bs = mx;
-      se = ns;
-      lse_merge(tm, tse, sx[0][w], sx[1][w]);
-    }
-    const float ts_lse = bs == -INFINITY ? -INFINITY : bs + __logf(se);
-    s_mask_text = (bs > -INFINITY && ts_lse > bt) ? 1 : 0;   // timestamp mass wins: text masked
-    s_tm = tm; s_ts = tse; s_bt = bt; s_bs = bs;
-    sv[0][2] = se;
-    si[0][0] = it; si[0][1] = is;
+    const float ts_lse = a.bs == -INFINITY ? -INFINITY : a.bs + __logf(a.se);
+    s_mask_text = (a.bs > -INFINITY && ts_lse > a.bt) ? 1 : 0;   // timestamp mass wins: text masked
   }
   __syncthreads();
   const bool mask_text = s_mask_text != 0;
@@ -437,19 +534,18 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
   if (sample) {                                          // second pass: Gumbel-max over the processed row
     float sb = -INFINITY;
     for_row(p, row, [&](int v, float x, bool sup, bool beg) {
-      if (masked(v, sup, beg) || !(x > -INFINITY) || (mask_text && v < q.ts_begin)) return;
+      if (ts_masked(q, r, v, sup, beg) || !(x > -INFINITY) || (mask_text && v < q.ts_begin)) return;
       const float g = x * inv_t + gumbel(seed, b, p.col, v);
       if (g > sb || (g == sb && v < spick)) { sb = g; spick = v; }
     });
     block_argmax(sb, spick, sx, sxi, 2);
   }
   if (tid == 0) {
-    bt = s_bt; bs = s_bs; it = si[0][0]; is = si[0][1];
-    const float ts_l = lse_val(bs, sv[0][2]);
+    const float ts_l = lse_val(a.bs, a.se);
     int best;
-    if (mask_text) best = is;
-    else if (bt >= bs && it != 0x7fffffff) best = it;                 // text ids < timestamp ids: ties -> text
-    else if (is != 0x7fffffff) best = is;
+    if (mask_text) best = a.is;
+    else if (a.bt >= a.bs && a.it != 0x7fffffff) best = a.it;       // text ids < timestamp ids: ties -> text
+    else if (a.is != 0x7fffffff) best = a.is;
     else best = 0;
     if (sample) best = spick == 0x7fffffff ? best : spick;
     const bool fin = p.done[b] != 0;
@@ -461,13 +557,60 @@ __global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q) {
     if (p.sum_logp && !fin) {
       float lse = ts_l;
       if (!mask_text) {
-        float m = s_tm, ss = s_ts;
-        if (bs > -INFINITY) lse_merge(m, ss, bs, sv[0][2]);
+        float m = a.tm, ss = a.tse;
+        if (a.bs > -INFINITY) lse_merge(m, ss, a.bs, a.se);
         lse = lse_val(m, ss);
       }
       p.sum_logp[b] += to_f32(row[best]) - lse;
     }
   }
+}
+
+// grid (G, B): G == 1 -> whole row + finish; G > 1 -> partial of slice blockIdx.x into ws
+template <typename E>
+__global__ __launch_bounds__(256) void greedy_select_ts_kernel(SelTsP q, int slice, float* ws) {
+  __shared__ float sv[4][8];
+  __shared__ int si[4][2];
+  __shared__ float sx[4][4];
+  __shared__ int sxi[4][4];
+  const int g = blockIdx.x, G = gridDim.x, b = blockIdx.y;
+  if (q.s.t_dev) q.s.col += *q.s.t_dev;
+  const TsRow r = ts_row(q, b);
+  const bool lse = q.s.sum_logp != nullptr;
+  const E* row = (const E*)q.s.logits + b * q.s.ld;
+  TsAcc a;
+  ts_init(a);
+  const int lo = G == 1 ? 0 : g * slice, hi = G == 1 ? q.s.V : min(q.s.V, lo + slice);
+  ts_scan(q, r, row, a, lo, hi);
+  ts_block(a, lse, sv, si);
+  if (G == 1) {
+    ts_finish<E>(q, r, b, a, sx, sxi);
+  } else if (threadIdx.x == 0) {
+    float* w = ws + ((int64_t)b * G + g) * SEL_WORDS;
+    w[0] = a.bt; w[1] = a.bs; w[2] = a.se; w[3] = a.tm; w[4] = a.tse;
+    w[5] = __int_as_float(a.it); w[6] = __int_as_float(a.is);
+  }
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void ts_merge_kernel(SelTsP q, int G, const float* ws) {
+  __shared__ float sx[4][4];
+  __shared__ int sxi[4][4];
+  const int b = blockIdx.x;
+  if (q.s.t_dev) q.s.col += *q.s.t_dev;
+  const TsRow r = ts_row(q, b);
+  const bool lse = q.s.sum_logp != nullptr;
+  TsAcc a;
+  ts_init(a);
+  if (threadIdx.x == 0)
+    for (int g = 0; g < G; ++g) {
+      const float* w = ws + ((int64_t)b * G + g) * SEL_WORDS;
+      TsAcc o;
+      o.bt = w[0]; o.bs = w[1]; o.se = w[2]; o.tm = w[3]; o.tse = w[4];
+      o.it = __float_as_int(w[5]); o.is = __float_as_int(w[6]);
+      ts_merge(a, o, lse);
+    }
+  ts_finish<E>(q, r, b, a, sx, sxi);
 }
 
 // out[b] = log_softmax(logits[b, :V])[token]   (fp32 of the bf16 / fp32 row)
@@ -528,6 +671,43 @@ int sel_vec(const void* logits, int64_t ld, int V) {
     else return TW_EUNSUPPORTED;                                                            \
   } while (0)
 
+// slices per row: enough workgroups to cover the chip for a handful of rows, one per row from 256 rows
+// up; the slices are multiples of 8 ids (for_row's 16-B chunks)
+int sel_slices(int B, int V) {
+  int G = 1;
+  while (G < 32 && (int64_t)B * G * 2 <= 512) G *= 2;
+  const int slice = ((V + G - 1) / G + 7) / 8 * 8;
+  return (V + slice - 1) / slice;
+}
+
+int launch_select(const SelP& p, int B, int logits_dtype, hipStream_t stream) {
+  const int G = sel_slices(B, p.V);
+  const int slice = ((p.V + G - 1) / G + 7) / 8 * 8;
+  float* ws = G > 1 ? (float*)tw_device_workspace(stream, (size_t)B * G * SEL_WORDS * sizeof(float)) : nullptr;
+  if (G > 1 && ws) {
+    TW_LAUNCH_DT(logits_dtype, greedy_select_kernel, dim3(G, B), dim3(256), p, slice, ws);
+    TW_LAUNCH_DT(logits_dtype, greedy_merge_kernel, dim3(B), dim3(64), p, G, ws);
+  } else {
+    TW_LAUNCH_DT(logits_dtype, greedy_select_kernel, dim3(1, B), dim3(256), p, p.V, (float*)nullptr);
+  }
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+int launch_select_ts(const SelTsP& q, int B, int logits_dtype, hipStream_t stream) {
+  const int G = sel_slices(B, q.s.V);
+  const int slice = ((q.s.V + G - 1) / G + 7) / 8 * 8;
+  float* ws = G > 1 ? (float*)tw_device_workspace(stream, (size_t)B * G * SEL_WORDS * sizeof(float)) : nullptr;
+  if (G > 1 && ws) {
+    TW_LAUNCH_DT(logits_dtype, greedy_select_ts_kernel, dim3(G, B), dim3(256), q, slice, ws);
+    TW_LAUNCH_DT(logits_dtype, ts_merge_kernel, dim3(B), dim3(256), q, G, ws);
+  } else {
+    TW_LAUNCH_DT(logits_dtype, greedy_select_ts_kernel, dim3(1, B), dim3(256), q, q.s.V, (float*)nullptr);
+  }
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
 }  // namespace
 
 extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
@@ -543,9 +723,7 @@ extern "C" int tw_greedy_select_ts(const void* logits, int64_t ld, int logits_dt
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
   q.s.ctl = nullptr; q.s.sum_logp = nullptr; q.s.vec = sel_vec(logits, ld, V);
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
-  TW_LAUNCH_DT(logits_dtype, greedy_select_ts_kernel, dim3(B), dim3(256), q);
-  TW_CHECK_LAUNCH();
-  return TW_OK;
+  return launch_select_ts(q, B, logits_dtype, stream);
 }
 
 extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
@@ -563,9 +741,7 @@ extern "C" int tw_select_sample_ts(const void* logits, int64_t ld, int logits_dt
   q.s.t_dev = t_dev; q.s.begin_col = begin_col;
   q.s.ctl = ctl; q.s.sum_logp = sum_logp; q.s.vec = sel_vec(logits, ld, V);
   q.begin_col = begin_col; q.ts_begin = ts_begin; q.no_ts = no_ts; q.max_initial = max_initial; q.last_ts = last_ts;
-  TW_LAUNCH_DT(logits_dtype, greedy_select_ts_kernel, dim3(B), dim3(256), q);
-  TW_CHECK_LAUNCH();
-  return TW_OK;
+  return launch_select_ts(q, B, logits_dtype, stream);
 }
 
 extern "C" int tw_token_logprob(const void* logits, int64_t ld, int logits_dtype, int B, int V, int token,
@@ -645,7 +821,7 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   const int nchunk = tk_dev ? DA_MAX_TK / DA_SPLIT : (Tk + DA_SPLIT - 1) / DA_SPLIT;
   const bool split = tk_dev ? split_mode == 3 && B * H < 640
                             : split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
-  if (split && nchunk >= 2) {
+  if (split && nchunk >= 2 && nchunk <= DA_MAX_CHUNK) {
     float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
     if (ws) {
       TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws);
@@ -671,9 +847,7 @@ extern "C" int tw_greedy_select(const void* logits, int64_t ld, int logits_dtype
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
   p.ctl = nullptr; p.sum_logp = nullptr; p.vec = sel_vec(logits, ld, V);
-  TW_LAUNCH_DT(logits_dtype, greedy_select_kernel, dim3(B), dim3(256), p);
-  TW_CHECK_LAUNCH();
-  return TW_OK;
+  return launch_select(p, B, logits_dtype, stream);
 }
 
 extern "C" int tw_select_sample(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
@@ -689,7 +863,5 @@ extern "C" int tw_select_sample(const void* logits, int64_t ld, int logits_dtype
   p.eos = eos; p.done = done; p.ids = ids; p.ld_ids = ld_ids; p.col = col; p.next = next_ids;
   p.t_dev = t_dev; p.begin_col = begin_col;
   p.ctl = ctl; p.sum_logp = sum_logp; p.vec = sel_vec(logits, ld, V);
-  TW_LAUNCH_DT(logits_dtype, greedy_select_kernel, dim3(B), dim3(256), p);
-  TW_CHECK_LAUNCH();
-  return TW_OK;
+  return launch_select(p, B, logits_dtype, stream);
 }

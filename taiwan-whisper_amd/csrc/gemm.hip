@@ -501,13 +501,26 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmP p, int S) {
 // applies the full epilogue (epi_element).  Fusing the LN removes one launch per LN'd Linear, which is
 // most of a batch-1 step's cost (every launch there is latency-bound).
 // ---------------------------------------------------------------------------------------------
-template <int MR>
+template <int MR, int CPW>
 __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                    float eps) {
   extern __shared__ __attribute__((aligned(16))) char gemv_smem[];
   bf16* xs = (bf16*)gemv_smem;                         // [MR][K] bf16
   const int lane = lane_id(), wave = wave_id_uniform();
   const int K = p.K;
+  // this wave's W rows (CPW output columns): the first (up to) GV_PRE 16-B pieces per lane are loaded
+  // before the A rows are staged, so their HBM latency hides behind the LayerNorm / LDS prologue
+  constexpr int GV_PRE = CPW == 1 ? 12 : 3;
+  const int n0 = (blockIdx.x * 4 + wave) * CPW;
+  bf16x8 wpre[CPW][GV_PRE];
+  const int npre = min(GV_PRE, (K - lane * 8 + 511) / 512);
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    const int n = n0 + c;
+    const bf16* wr = p.B + (int64_t)(n < p.N ? n : 0) * p.ldb;
+#pragma unroll
+    for (int u = 0; u < GV_PRE; ++u) wpre[c][u] = (u < npre) ? *(const bf16x8*)(wr + lane * 8 + u * 512) : bf16x8{};
+  }
   if (wave < MR) {
     bf16* dst = xs + (int64_t)wave * K;
     if (wave >= p.M) {
@@ -557,34 +570,49 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
     }
   }
   __syncthreads();
-  const int n = blockIdx.x * 4 + wave;
-  if (n >= p.N) return;
-  const bf16* wr = p.B + (int64_t)n * p.ldb;
-  float acc[MR];
+  if (n0 >= p.N) return;
+  float acc[CPW][MR];
 #pragma unroll
-  for (int r = 0; r < MR; ++r) acc[r] = 0.f;
-  for (int k0 = lane * 8; k0 < K; k0 += 4 * 512) {
-    bf16x8 w8[4];
+  for (int c = 0; c < CPW; ++c)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) w8[u] = (k0 + u * 512 < K) ? *(const bf16x8*)(wr + k0 + u * 512) : bf16x8{};
+    for (int r = 0; r < MR; ++r) acc[c][r] = 0.f;
+  // k order per lane: pieces u = 0, 1, ... at k = lane*8 + 512u (the preloaded ones first, the rest streamed)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (k0 + u * 512 < K) {
+  for (int u = 0; u < GV_PRE; ++u) {
+    if (u < npre) {
 #pragma unroll
-        for (int r = 0; r < MR; ++r) {
-          const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + k0 + u * 512);
+      for (int r = 0; r < MR; ++r) {
+        const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + lane * 8 + u * 512);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc[r] = fmaf(bf2f(w8[u][q]), bf2f(a8[q]), acc[r]);
-        }
+        for (int c = 0; c < CPW; ++c)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(bf2f(wpre[c][u][q]), bf2f(a8[q]), acc[c][r]);
+      }
+    }
+  }
+  for (int k0 = lane * 8 + GV_PRE * 512; k0 < K; k0 += 512) {
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int n = n0 + c;
+      const bf16x8 w8 = *(const bf16x8*)(p.B + (int64_t)(n < p.N ? n : 0) * p.ldb + k0);
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + k0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(bf2f(w8[q]), bf2f(a8[q]), acc[c][r]);
       }
     }
   }
 #pragma unroll
-  for (int r = 0; r < MR; ++r) acc[r] = wave_sum(acc[r]);
+  for (int c = 0; c < CPW; ++c)
+#pragma unroll
+    for (int r = 0; r < MR; ++r) acc[c][r] = wave_sum(acc[c][r]);
   if (lane == 0)
 #pragma unroll
-    for (int r = 0; r < MR; ++r)
-      if (r < p.M) epi_element(p, r, n, acc[r]);
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int r = 0; r < MR; ++r)
+        if (r < p.M && n0 + c < p.N) epi_element(p, r, n0 + c, acc[c][r]);
 }
 
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
@@ -686,6 +714,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // pointer of an older block, so old blocks are kept) outside stream capture only.  GEMMs of one
 // device are issued from one stream at a time (the trainer's and the decoder's current stream).
 void* splitk_workspace(hipStream_t stream, size_t bytes) {
+  // at least 4 MiB per allocation: the small users (decode-attention partials, selection partials) then
+  // find the block already large enough inside a captured decode step once any eager call has run
+  bytes = std::max(bytes, (size_t)4 << 20);
   static std::mutex mu;
   static std::vector<std::pair<int, std::pair<void*, size_t>>> cur;   // device -> (ptr, bytes)
   int dev = 0;
@@ -862,13 +893,21 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
   p.alpha = 1.f; p.bias = (const bf16*)bias;
   p.res = res; p.ldr = ldr; p.res_dtype = res_dtype; p.res_mod = 0;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.c_dtype = c_dtype; p.flags = flags;
-  const dim3 grid((N + 3) / 4);
-  if (M == 1)
-    hipLaunchKernelGGL(gemv_kernel<1>, grid, dim3(256), (size_t)K * 2, stream, p, ln_w, ln_b, eps);
-  else if (M == 2)
-    hipLaunchKernelGGL(gemv_kernel<2>, grid, dim3(256), (size_t)2 * K * 2, stream, p, ln_w, ln_b, eps);
-  else
-    hipLaunchKernelGGL(gemv_kernel<4>, grid, dim3(256), (size_t)4 * K * 2, stream, p, ln_w, ln_b, eps);
+  // one output column per wave, or 8 for very wide N (the LM head: fewer workgroups repeating the A prologue)
+  const int cpw = N >= 16384 ? 8 : 1;
+  const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
+  const size_t lds = (size_t)(M == 1 ? 1 : M == 2 ? 2 : 4) * K * 2;
+#define TW_GEMV(MR_, CPW_) hipLaunchKernelGGL((gemv_kernel<MR_, CPW_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps)
+  if (cpw == 8) {
+    if (M == 1) TW_GEMV(1, 8);
+    else if (M == 2) TW_GEMV(2, 8);
+    else TW_GEMV(4, 8);
+  } else {
+    if (M == 1) TW_GEMV(1, 1);
+    else if (M == 2) TW_GEMV(2, 1);
+    else TW_GEMV(4, 1);
+  }
+#undef TW_GEMV
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
