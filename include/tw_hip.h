@@ -99,10 +99,13 @@ int tw_logmel_len(const float* wav, int B, int64_t n_samples, const float* basis
 int tw_mel_to_conv_input(const float* mel, void* xt, int B, int nmel, int T, tw_stream_t stream);
 
 /* Decoder token + learned position embedding (HF modeling_whisper.py:736,754-761) and its
- * scatter-add backward into the tied embedding gradient. */
+ * backward into the tied embedding gradient: deterministic (rows of one id summed in position order,
+ * one writer per id); positions whose id == padding_idx add nothing (nn.Embedding's padding_idx,
+ * = config.pad_token_id in HF WhisperDecoder; -1: none).  Scratch: the per-device block. */
 int tw_embed_fwd(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
                  int out_dtype, int rows, int T, int pos_offset, int D, tw_stream_t stream);
-int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D, tw_stream_t stream);
+int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D, int64_t padding_idx,
+                 tw_stream_t stream);
 
 /* autocast weight cast fp32 -> bf16 (ACC:accelerator.py autocast of every Linear weight). */
 int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, tw_stream_t stream);

@@ -6,7 +6,11 @@ kernel stages operands with 16-B buffer_load ... lds); WRITE_SIZE is exact for 1
 8-B stores are uncalibrated).  Infinity-Cache hits appear to be counted, so this is an upper bound
 of DRAM bytes.
 
-usage: python pmc_summary.py <fetch_dir> <write_dir> <out.json>
+A third, optional pass (TCC_EA0_RDREQ_sum + TCC_EA0_RDREQ_DRAM_sum: the L2's memory-side read requests and
+the share of them destined for DRAM rather than served by the Infinity Cache) splits the fetched bytes
+into DRAM and MALL: dram_fetch_bytes = fetch x RDREQ_DRAM / RDREQ.
+
+usage: python pmc_summary.py <fetch_dir> <write_dir> <out.json> [<dram_dir>]
 """
 import csv
 import json
@@ -38,7 +42,10 @@ def load(d, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    ddir = sys.argv[4] if len(sys.argv) > 4 else None
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    rq = load(ddir, "TCC_EA0_RDREQ_sum") if ddir else {}
+    rqd = load(ddir, "TCC_EA0_RDREQ_DRAM_sum") if ddir else {}
     res = {}
     for fam in FAMILIES:
         if not fetch.get(fam) or not write.get(fam):
@@ -47,9 +54,17 @@ def main():
         w = sum(write[fam]) / len(write[fam]) * 1024
         res[fam] = dict(launches=len(fetch[fam]), fetch_bytes_per_launch=f, write_bytes_per_launch=w,
                         hbm_bytes_per_launch=f + w)
-        print(f"{fam:9s} launches={len(fetch[fam]):5d} fetch {f/1e6:9.1f} MB  write {w/1e6:9.1f} MB per launch")
+        extra = ""
+        if rq.get(fam) and rqd.get(fam) and sum(rq[fam]) > 0:
+            share = sum(rqd[fam]) / sum(rq[fam])
+            res[fam]["dram_read_share"] = share
+            res[fam]["dram_fetch_bytes_per_launch"] = f * share
+            res[fam]["dram_bytes_per_launch"] = f * share + w
+            extra = f"  DRAM share of reads {share:.3f} -> {f * share / 1e6:9.1f} MB from DRAM"
+        print(f"{fam:9s} launches={len(fetch[fam]):5d} fetch {f/1e6:9.1f} MB  write {w/1e6:9.1f} MB per launch{extra}")
     res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over `bench.py --steps 2 --warmup 1`; "
-                    "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes")
+                    "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; the fetch counts Infinity-Cache hits too "
+                    "(MI355X_MICROARCH.md): dram_* split it by TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ from a third pass")
     json.dump(res, open(out, "w"), indent=1)
 
 

@@ -31,7 +31,7 @@ SIGNATURES = {
     "tw_logmel_len": [P, I32, I64, P, P, P, P, P, P, P],
     "tw_mel_to_conv_input": [P, P, I32, I32, I32, P],
     "tw_embed_fwd": [P, P, I32, P, I32, P, I32, I32, I32, I32, I32, P],
-    "tw_embed_bwd": [P, P, P, I32, I32, P],
+    "tw_embed_bwd": [P, P, P, I32, I32, I64, P],
     "tw_cast_f32_bf16": [P, P, I64, P],
     "tw_colsum": [P, I32, I64, I32, I32, P, I32, I32, P, I64, P],
     "tw_l2norm": [P, I64, P, P, P],

@@ -788,7 +788,8 @@ class Backward:
                 self._layer_done(p)
             elif kind == "embed":
                 if gE is not None:
-                    F.embed_bwd(st["ids"], dx, gE)
+                    # HF's decoder embed_tokens has padding_idx = pad_token_id: pad positions add nothing
+                    F.embed_bwd(st["ids"], dx, gE, padding_idx=m.config.pad_token_id)
                 gP = m.gv("model.decoder.embed_positions.weight")
                 if gP is not None:   # sum over the batch of position rows
                     F.colsum(dx, st["T"] * d, st["B"], st["T"] * d, gP.view(-1), accum=True, round_bf16=False)

@@ -225,11 +225,13 @@ def embed_fwd(ids, tok, pos, out, T, pos_offset=0):
     return out
 
 
-def embed_bwd(ids, dh, dE):
+def embed_bwd(ids, dh, dE, padding_idx=-1):
+    """dE[id] += sum of dh rows with that id (position order); ids == padding_idx skipped (nn.Embedding)."""
     rows = ids.numel()
     D = dE.shape[1]
     assert dh.dtype == torch.float32 and dE.dtype == torch.float32 and dh.numel() == rows * D
-    call("tw_embed_bwd", ids.data_ptr(), dh.data_ptr(), dE.data_ptr(), rows, D, _stream())
+    assert ids.dtype == torch.int64 and ids.is_contiguous()
+    call("tw_embed_bwd", ids.data_ptr(), dh.data_ptr(), dE.data_ptr(), rows, D, int(padding_idx), _stream())
 
 
 def cast_bf16(src, dst):

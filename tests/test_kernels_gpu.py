@@ -635,6 +635,12 @@ def test_embed_adamw_norm_shift():
         ops.embed_bwd(ids2.to(DEV), dh2.to(DEV), dE2)
         outs.append(dE2.cpu())
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], want)
+    # padding_idx (nn.Embedding(..., padding_idx)): rows of that id add nothing, the rest unchanged
+    dE3 = base.to(DEV).clone()
+    ops.embed_bwd(ids2.to(DEV), dh2.to(DEV), dE3, padding_idx=7)
+    want3 = want.clone()
+    want3[7] = base[7]
+    assert torch.equal(dE3.cpu(), want3)
     # clip + AdamW vs torch
     n = 10007
     p0, gr = torch.randn(n, generator=g), torch.randn(n, generator=g) * 3
