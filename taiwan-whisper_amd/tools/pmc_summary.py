@@ -6,9 +6,10 @@ kernel stages operands with 16-B buffer_load ... lds); WRITE_SIZE is exact for 1
 8-B stores are uncalibrated).  Infinity-Cache hits appear to be counted, so this is an upper bound
 of DRAM bytes.
 
-A third, optional pass (TCC_EA0_RDREQ_sum + TCC_EA0_RDREQ_DRAM_sum: the L2's memory-side read requests and
-the share of them destined for DRAM rather than served by the Infinity Cache) splits the fetched bytes
-into DRAM and MALL: dram_fetch_bytes = fetch x RDREQ_DRAM / RDREQ.
+A third, optional pass records TCC_EA0_RDREQ_sum and TCC_EA0_RDREQ_DRAM_sum (read requests "destined for
+DRAM").  Measured r02: the two are equal for every kernel family (share 1.000), i.e. the counter is taken
+before the Infinity Cache (MALL), so it does not split MALL hits from HBM reads; fetch stays an upper
+bound of DRAM bytes.
 
 usage: python pmc_summary.py <fetch_dir> <write_dir> <out.json> [<dram_dir>]
 """
