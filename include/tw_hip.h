@@ -55,11 +55,13 @@ int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t
  * A is bit-identical to tw_layernorm_fwd's bf16 output, so an LN launch + GEMM pair becomes one launch).
  * Replaces, per decode step, HF WhisperDecoderLayer's LayerNorm + nn.Linear pairs and the plain Linears
  * (modeling_whisper.py:448-506) for a batch of <= 4.  W [N][K] bf16; flags / bias / res / aux as
- * tw_gemm_bf16 (F_BIAS, F_ROUND, F_GELU, F_RES, F_AUX_OUT, F_ACCUM); C fp32 or bf16. */
+ * tw_gemm_bf16 (F_BIAS, F_ROUND, F_GELU, F_RES, F_AUX_OUT, F_ACCUM); C fp32 or bf16.  kv_cache != NULL fuses
+ * tw_kv_append: columns n >= kv_col0 are also stored at kv_cache[m*kv_sb + (*t_dev)*kv_ld + n - kv_col0]
+ * (the self-attention K/V row of the step, the fused QKV projection's k | v part). */
 int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
                  int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
                  const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
-                 tw_stream_t stream);
+                 void* kv_cache, int64_t kv_sb, int64_t kv_ld, int kv_col0, const int* t_dev, tw_stream_t stream);
 
 /* LayerNorm fp32-statistics forward / backward (D % 64 == 0, D <= 1280).
  * Replaces nn.LayerNorm at HF modeling_whisper.py:392,402,470,485,498,642,790 (autocast fp32 op). */

@@ -158,39 +158,19 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
 
 // split over keys (few (clip, head) pairs: batch-1 long-form): blockIdx.y = chunk of S keys; chunks past
 // the effective Tk store an empty partial (m = -inf, l = 0)
-template <typename E>
-__global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, int S, float* ws) {
-  const int bh = blockIdx.x, c = blockIdx.y;
-  const int b = bh / p.H, h = bh % p.H;
-  int tk = p.Tk + (p.tk_dev ? *p.tk_dev : 0);
-  if (tk > DA_MAX_TK) tk = DA_MAX_TK;
-  float* part = ws + ((int64_t)bh * gridDim.y + c) * 66;
-  const int lo = c * S, hi = min(tk, lo + S);
-  if (lo >= hi) {
-    if (threadIdx.x < 64) part[threadIdx.x] = 0.f;
-    if (threadIdx.x == 0) {
-      part[64] = -INFINITY;
-      part[65] = 0.f;
-    }
-    return;
-  }
-  decode_attn_body<E>(p, b, h, lo, hi, part);
-}
-
-// O = sum_c 2^(m_c - M) o_c / sum_c 2^(m_c - M) l_c over the chunks of one (clip, head), in chunk order.
-// Lane c loads chunk c's (m, l) and every lane its column of all chunks up front (nchunk <= DA_MAX_CHUNK
-// independent loads in flight instead of a dependent chain), weights broadcast by shuffles.
+// O = sum_c 2^(m_c - M) o_c / sum_c 2^(m_c - M) l_c over the chunks of one (clip, head), in chunk order,
+// by the 64 lanes of one wave (lane = output dimension).  Lane c loads chunk c's (m, l) and every lane its
+// column of all chunks up front (independent loads instead of a dependent chain), weights by shuffles.
 constexpr int DA_MAX_CHUNK = 16;
 template <typename E>
-__global__ __launch_bounds__(64) void decode_attn_combine_kernel(DecP p, int nchunk, const float* ws) {
-  const int bh = blockIdx.x, tid = threadIdx.x;
+__device__ __forceinline__ void combine_row(const DecP& p, int bh, int nchunk, const float* part) {
+  const int lane = threadIdx.x & 63;
   const int b = bh / p.H, h = bh % p.H;
-  const float* part = ws + (int64_t)bh * nchunk * 66;
-  const float mc = tid < nchunk ? part[tid * 66 + 64] : -INFINITY;
-  const float lc = tid < nchunk ? part[tid * 66 + 65] : 0.f;
+  const float mc = lane < nchunk ? part[lane * 66 + 64] : -INFINITY;
+  const float lc = lane < nchunk ? part[lane * 66 + 65] : 0.f;
   float oc[DA_MAX_CHUNK];
 #pragma unroll
-  for (int c = 0; c < DA_MAX_CHUNK; ++c) oc[c] = c < nchunk ? part[c * 66 + tid] : 0.f;
+  for (int c = 0; c < DA_MAX_CHUNK; ++c) oc[c] = c < nchunk ? part[c * 66 + lane] : 0.f;
   const float M = wave_max(mc);
   const float wc = mc == -INFINITY ? 0.f : (sizeof(E) == 4 ? exp2f(mc - M) : __builtin_amdgcn_exp2f(mc - M));
   float acc = 0.f, lt = 0.f;
@@ -204,7 +184,64 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(DecP p, int nch
       }
     }
   }
-  from_f32(((E*)p.o)[b * p.sob + h * 64 + tid], acc / lt);
+  from_f32(((E*)p.o)[b * p.sob + h * 64 + lane], acc / lt);
+}
+
+// split over keys (few (clip, head) pairs: batch-1 long-form): blockIdx.y = chunk of S keys; chunks past
+// the effective Tk store an empty partial (m = -inf, l = 0).  With `counters` the chunk that finishes
+// last for its (clip, head) combines them (no second launch): wave 0 (which stored the partial) releases
+// it at agent scope and counts it with an agent-scope atomic; the wave that sees the count reach the
+// chunk count acquires, combines, and resets the counter for the next launch.  No wave ever waits on
+// another (no spinning), so the kernel cannot stall on a lost update.
+template <typename E>
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, int S, float* ws, unsigned* counters) {
+  const int bh = blockIdx.x, c = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  int tk = p.Tk + (p.tk_dev ? *p.tk_dev : 0);
+  if (tk > DA_MAX_TK) tk = DA_MAX_TK;
+  float* part = ws + ((int64_t)bh * gridDim.y + c) * 66;
+  const int lo = c * S, hi = min(tk, lo + S);
+  if (lo >= hi) {
+    if (threadIdx.x < 64) part[threadIdx.x] = 0.f;
+    if (threadIdx.x == 0) {
+      part[64] = -INFINITY;
+      part[65] = 0.f;
+    }
+  } else {
+    decode_attn_body<E>(p, b, h, lo, hi, part);
+  }
+  if (!counters || threadIdx.x >= 64) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  unsigned prev = 0;
+  if (threadIdx.x == 0) prev = __hip_atomic_fetch_add(counters + bh, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0, 64);
+  if (prev != gridDim.y - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  combine_row<E>(p, bh, gridDim.y, ws + (int64_t)bh * gridDim.y * 66);
+  if (threadIdx.x == 0) __hip_atomic_store(counters + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename E>
+__global__ __launch_bounds__(64) void decode_attn_combine_kernel(DecP p, int nchunk, const float* ws) {
+  combine_row<E>(p, blockIdx.x, nchunk, ws + (int64_t)blockIdx.x * nchunk * 66);
+}
+
+// per-device zeroed arrival counters of the split kernel (allocated and cleared outside stream capture,
+// reset by the kernel itself after every use)
+constexpr int DA_MAX_COUNTERS = 4096;
+unsigned* split_counters(hipStream_t stream) {
+  static unsigned* ctr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (ctr[dev]) return ctr[dev];
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cap);
+  if (cap != hipStreamCaptureStatusNone) return nullptr;
+  unsigned* c = nullptr;
+  if (hipMalloc(&c, DA_MAX_COUNTERS * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemset(c, 0, DA_MAX_COUNTERS * sizeof(unsigned)) != hipSuccess) return nullptr;
+  ctr[dev] = c;
+  return c;
 }
 
 struct SelP {
@@ -823,9 +860,12 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
                             : split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
   if (split && nchunk >= 2 && nchunk <= DA_MAX_CHUNK) {
     float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
+    // TW_DECODE_COMBINE=2 (A/B): always the separate combine launch
+    static const int combine_mode = [] { const char* e = getenv("TW_DECODE_COMBINE"); return e ? atoi(e) : 1; }();
+    unsigned* ctr = (combine_mode != 2 && B * H <= DA_MAX_COUNTERS) ? split_counters(stream) : nullptr;
     if (ws) {
-      TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws);
-      TW_LAUNCH_DT(dtype, decode_attn_combine_kernel, dim3(B * H), dim3(64), p, nchunk, ws);
+      TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws, ctr);
+      if (!ctr) TW_LAUNCH_DT(dtype, decode_attn_combine_kernel, dim3(B * H), dim3(64), p, nchunk, ws);
       TW_CHECK_LAUNCH();
       return TW_OK;
     }

@@ -383,7 +383,8 @@ void launch(GemmP p, int batch, hipStream_t stream) {
 // once per step), A fragments from L2 (A is at most 128 x K bf16), MFMA 16x16x32 with swapped
 // operands, the 4 wave partials summed through LDS, then the per-element epilogue (every flag).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float v) {
+// the epilogue value of C[m][n] (writes the GELU pre-activation to aux on the way), before the store
+__device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v) {
   const int flags = p.flags;
   v *= p.alpha;
   if (flags & F_BIAS) v += bf2f(p.bias[n]);
@@ -397,8 +398,13 @@ __device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float 
     const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
     v += ld_as_f32(p.res, p.res_dtype, (int64_t)mr * p.ldr + n);
   }
+  if (flags & F_ACCUM) v += ld_as_f32(p.C, p.c_dtype, (int64_t)m * p.ldc + n);
+  return v;
+}
+
+__device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float v) {
+  v = epi_value(p, m, n, v);
   const int64_t co = (int64_t)m * p.ldc + n;
-  if (flags & F_ACCUM) v += ld_as_f32(p.C, p.c_dtype, co);
   if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2bf(v);
   else ((float*)p.C)[co] = v;
 }
@@ -501,9 +507,19 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmP p, int S) {
 // applies the full epilogue (epi_element).  Fusing the LN removes one launch per LN'd Linear, which is
 // most of a batch-1 step's cost (every launch there is latency-bound).
 // ---------------------------------------------------------------------------------------------
+// Optional KV-cache append fused into the epilogue (the decode step's QKV projection): output columns
+// n >= kv.col0 are also stored at kv.cache[m * kv.sb + (*kv.t) * kv.ld + n - kv.col0] -- what tw_kv_append
+// copies, one launch fewer per decoder layer.
+struct GemvKV {
+  void* cache;
+  int64_t sb, ld;
+  int col0;
+  const int* t;
+};
+
 template <int MR, int CPW>
 __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                   float eps) {
+                                                   float eps, GemvKV kv) {
   extern __shared__ __attribute__((aligned(16))) char gemv_smem[];
   bf16* xs = (bf16*)gemv_smem;                         // [MR][K] bf16
   const int lane = lane_id(), wave = wave_id_uniform();
@@ -607,12 +623,26 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
   for (int c = 0; c < CPW; ++c)
 #pragma unroll
     for (int r = 0; r < MR; ++r) acc[c][r] = wave_sum(acc[c][r]);
-  if (lane == 0)
+  if (lane == 0) {
+    const int64_t t = kv.cache ? (int64_t)*kv.t : 0;
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
 #pragma unroll
-      for (int r = 0; r < MR; ++r)
-        if (r < p.M && n0 + c < p.N) epi_element(p, r, n0 + c, acc[c][r]);
+      for (int r = 0; r < MR; ++r) {
+        const int n = n0 + c;
+        if (r < p.M && n < p.N) {
+          const float v = epi_value(p, r, n, acc[c][r]);
+          const int64_t co = (int64_t)r * p.ldc + n;
+          if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2bf(v);
+          else ((float*)p.C)[co] = v;
+          if (kv.cache && n >= kv.col0) {
+            const int64_t ko = r * kv.sb + t * kv.ld + (n - kv.col0);
+            if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2bf(v);
+            else ((float*)kv.cache)[ko] = v;
+          }
+        }
+      }
+  }
 }
 
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
@@ -877,6 +907,7 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
 extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
                             int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
                             const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
+                            void* kv_cache, int64_t kv_sb, int64_t kv_ld, int kv_col0, const int* t_dev,
                             hipStream_t stream) {
   if (M <= 0 || N <= 0) return TW_OK;
   if (M > 4 || K <= 0 || (K % 8) || (ldx % 8) || (ldw % 8)) return TW_EINVAL;
@@ -887,6 +918,8 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
   if ((flags & (F_AUX_OUT | F_DGELU)) && !aux) return TW_EINVAL;
   if (c_dtype != TW_F32 && c_dtype != TW_BF16) return TW_EUNSUPPORTED;
   if ((size_t)4 * K * 2 > 64 * 1024) return TW_EUNSUPPORTED;        // A rows in LDS
+  if (kv_cache && (!t_dev || kv_col0 < 0 || kv_col0 >= N)) return TW_EINVAL;
+  const GemvKV kv{kv_cache, kv_sb, kv_ld, kv_col0, t_dev};
   GemmP p = {};
   p.A = (const bf16*)x; p.B = (const bf16*)W; p.C = C;
   p.lda = ldx; p.ldb = ldw; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
@@ -897,7 +930,7 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
   const int cpw = N >= 16384 ? 8 : 1;
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
   const size_t lds = (size_t)(M == 1 ? 1 : M == 2 ? 2 : 4) * K * 2;
-#define TW_GEMV(MR_, CPW_) hipLaunchKernelGGL((gemv_kernel<MR_, CPW_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps)
+#define TW_GEMV(MR_, CPW_) hipLaunchKernelGGL((gemv_kernel<MR_, CPW_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
   if (cpw == 8) {
     if (M == 1) TW_GEMV(1, 8);
     else if (M == 2) TW_GEMV(2, 8);

@@ -75,11 +75,13 @@ class DecodeSession:
         F.layernorm_fwd(x, m.ln_param(name + ".weight"), m.ln_param(name + ".bias"), self.y)
         return self.y
 
-    def _ln_lin(self, x, ln, w, b, out, flags=F.GEMM_ROUND):
-        """out = Linear(LayerNorm(x)): one GEMV launch (batch <= 4, bf16 stream) or LN + GEMM."""
+    def _ln_lin(self, x, ln, w, b, out, flags=F.GEMM_ROUND, kv=None):
+        """out = Linear(LayerNorm(x)): one GEMV launch (batch <= 4, bf16 stream) or LN + GEMM.  kv: the
+        GEMV also appends columns >= kv[3] to the self-attention cache row (only on the GEMV path)."""
         m = self.m
         if self.gemv_ln:
-            F.gemv(x, w, out, ln_w=m.ln_param(ln + ".weight"), ln_b=m.ln_param(ln + ".bias"), bias=b, flags=flags)
+            F.gemv(x, w, out, ln_w=m.ln_param(ln + ".weight"), ln_b=m.ln_param(ln + ".bias"), bias=b, flags=flags,
+                   kv=kv)
         else:
             y = self._ln(x, ln)
             if self.gemv:
@@ -111,9 +113,13 @@ class DecodeSession:
             # self attention: fused QKV -> staging; k, v appended at row t of the cache
             wqkv = m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d))
             bqkv = m.wspan(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,))
-            self._ln_lin(x, p + ".self_attn_layer_norm", wqkv, bqkv, self.qkv)
             cache = self.self_kv[i]
-            F.kv_append(self.qkv[:, d:], 3 * d, cache, 2 * d, sb, B, 2 * d, t_dev, T_max)
+            if self.gemv_ln:        # k, v of this step written to cache row t by the QKV GEMV itself
+                self._ln_lin(x, p + ".self_attn_layer_norm", wqkv, bqkv, self.qkv, kv=(cache, sb, 2 * d, d, t_dev,
+                                                                                     T_max))
+            else:
+                self._ln_lin(x, p + ".self_attn_layer_norm", wqkv, bqkv, self.qkv)
+                F.kv_append(self.qkv[:, d:], 3 * d, cache, 2 * d, sb, B, 2 * d, t_dev, T_max)
             F.decode_attn(self.qkv, 3 * d, cache, 2 * d, sb, cache.view(-1)[d:], 2 * d, sb, o, d, B, H, 1, 0.125,
                           tk_dev=t_dev, tk_max=T_max)
             self._lin(o, m._w16(p + ".self_attn.out_proj.weight"), m._w16(p + ".self_attn.out_proj.bias"), x, res=x)

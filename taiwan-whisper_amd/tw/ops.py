@@ -83,9 +83,10 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     return C
 
 
-def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=None, flags=0):
+def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=None, flags=0, kv=None):
     """tw_gemv_bf16: C[m] = epi(A[m] . W^T) for M <= 4 rows, A = x or LayerNorm(x) (ln_w / ln_b given):
-    the batch-1 decode step's LN + Linear pairs in one launch (include/tw_hip.h)."""
+    the batch-1 decode step's LN + Linear pairs in one launch (include/tw_hip.h).  kv = (cache, sb, ld, col0,
+    t_dev, t_max): columns >= col0 also go to cache row *t_dev (the fused KV append)."""
     M, K = x.shape
     N = W.shape[0]
     assert x.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and M <= 4 and W.shape[1] == K
@@ -102,10 +103,16 @@ def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=No
     if aux is not None:
         assert aux.dtype == torch.bfloat16
         _need(aux, (M - 1) * aux.stride(0) + N, "gemv aux")
+    kc, ksb, kld, kcol, kt = None, 0, 0, 0, None
+    if kv is not None:
+        kc, ksb, kld, kcol, kt, tmax = kv
+        assert kc.dtype == C.dtype and kt.dtype == torch.int32 and 0 <= kcol < N
+        _need(kc, (M - 1) * ksb + (tmax - 1) * kld + (N - kcol), "gemv kv cache")
     KernelTimer.wrap("gemv", 2.0 * M * N * K, lambda: call(
         "tw_gemv_bf16", x.data_ptr(), x.stride(0), _ptr(ln_w), _ptr(ln_b), float(eps), W.data_ptr(), K, C.data_ptr(),
         C.stride(0), _dt(C), M, N, K, _ptr(bias), _ptr(res), res.stride(0) if res is not None else 0,
-        _dt(res) if res is not None else F32, _ptr(aux), aux.stride(0) if aux is not None else 0, flags, _stream()))
+        _dt(res) if res is not None else F32, _ptr(aux), aux.stride(0) if aux is not None else 0, flags,
+        _ptr(kc), ksb, kld, kcol, _ptr(kt), _stream()))
     return C
 
 

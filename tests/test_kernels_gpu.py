@@ -581,6 +581,15 @@ def test_gemv_decode(M, N, K):
     else:
         y.copy_(xd)
         ops.gemv(y, Wd, C2, bias=bd, flags=ops.GEMM_ROUND)
+    # fused KV-cache append (the QKV projection of a decode step): columns >= col0 also land in row t
+    if N % 2 == 0:
+        col0, Tm, t = N // 3 // 8 * 8, 9, 5
+        cache = torch.zeros(M, Tm, N - col0, dtype=torch.bfloat16, device=DEV)
+        tdev = torch.tensor([t], dtype=torch.int32, device=DEV)
+        C3 = torch.empty_like(C2)
+        ops.gemv(y, Wd, C3, bias=bd, flags=ops.GEMM_ROUND, kv=(cache, Tm * (N - col0), N - col0, col0, tdev, Tm))
+        assert torch.equal(C3, C2) and torch.equal(cache[:, t], C2[:, col0:])
+        assert (cache[:, :t] == 0).all() and (cache[:, t + 1:] == 0).all()
     # GELU with the pre-activation output
     h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     pre = torch.empty_like(h)
