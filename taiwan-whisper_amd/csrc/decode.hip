@@ -188,13 +188,12 @@ __device__ __forceinline__ void combine_row(const DecP& p, int bh, int nchunk, c
 }
 
 // split over keys (few (clip, head) pairs: batch-1 long-form): blockIdx.y = chunk of S keys; chunks past
-// the effective Tk store an empty partial (m = -inf, l = 0).  With `counters` the chunk that finishes
-// last for its (clip, head) combines them (no second launch): wave 0 (which stored the partial) releases
-// it at agent scope and counts it with an agent-scope atomic; the wave that sees the count reach the
-// chunk count acquires, combines, and resets the counter for the next launch.  No wave ever waits on
-// another (no spinning), so the kernel cannot stall on a lost update.
+// the effective Tk store an empty partial (m = -inf, l = 0); decode_attn_combine_kernel merges them.
+// (Tried, r02: the last-arriving chunk combining in place -- agent-scope release + arrival counter --
+// saves the second launch at batch 1 (14.6 -> 13.7 us) but every workgroup's release writes back the
+// whole L2: 27 -> 202 us at B = 16, and c5 measured no faster.  Two launches it is.)
 template <typename E>
-__global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, int S, float* ws, unsigned* counters) {
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, int S, float* ws) {
   const int bh = blockIdx.x, c = blockIdx.y;
   const int b = bh / p.H, h = bh % p.H;
   int tk = p.Tk + (p.tk_dev ? *p.tk_dev : 0);
@@ -207,41 +206,14 @@ __global__ __launch_bounds__(DA_THREADS) void decode_attn_split_kernel(DecP p, i
       part[64] = -INFINITY;
       part[65] = 0.f;
     }
-  } else {
-    decode_attn_body<E>(p, b, h, lo, hi, part);
+    return;
   }
-  if (!counters || threadIdx.x >= 64) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  unsigned prev = 0;
-  if (threadIdx.x == 0) prev = __hip_atomic_fetch_add(counters + bh, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, 64);
-  if (prev != gridDim.y - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  combine_row<E>(p, bh, gridDim.y, ws + (int64_t)bh * gridDim.y * 66);
-  if (threadIdx.x == 0) __hip_atomic_store(counters + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  decode_attn_body<E>(p, b, h, lo, hi, part);
 }
 
 template <typename E>
 __global__ __launch_bounds__(64) void decode_attn_combine_kernel(DecP p, int nchunk, const float* ws) {
   combine_row<E>(p, blockIdx.x, nchunk, ws + (int64_t)blockIdx.x * nchunk * 66);
-}
-
-// per-device zeroed arrival counters of the split kernel (allocated and cleared outside stream capture,
-// reset by the kernel itself after every use)
-constexpr int DA_MAX_COUNTERS = 4096;
-unsigned* split_counters(hipStream_t stream) {
-  static unsigned* ctr[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (ctr[dev]) return ctr[dev];
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(stream, &cap);
-  if (cap != hipStreamCaptureStatusNone) return nullptr;
-  unsigned* c = nullptr;
-  if (hipMalloc(&c, DA_MAX_COUNTERS * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemset(c, 0, DA_MAX_COUNTERS * sizeof(unsigned)) != hipSuccess) return nullptr;
-  ctr[dev] = c;
-  return c;
 }
 
 struct SelP {
@@ -860,12 +832,9 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
                             : split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
   if (split && nchunk >= 2 && nchunk <= DA_MAX_CHUNK) {
     float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
-    // TW_DECODE_COMBINE=2 (A/B): always the separate combine launch
-    static const int combine_mode = [] { const char* e = getenv("TW_DECODE_COMBINE"); return e ? atoi(e) : 1; }();
-    unsigned* ctr = (combine_mode != 2 && B * H <= DA_MAX_COUNTERS) ? split_counters(stream) : nullptr;
     if (ws) {
-      TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws, ctr);
-      if (!ctr) TW_LAUNCH_DT(dtype, decode_attn_combine_kernel, dim3(B * H), dim3(64), p, nchunk, ws);
+      TW_LAUNCH_DT(dtype, decode_attn_split_kernel, dim3(B * H, nchunk), dim3(DA_THREADS), p, DA_SPLIT, ws);
+      TW_LAUNCH_DT(dtype, decode_attn_combine_kernel, dim3(B * H), dim3(64), p, nchunk, ws);
       TW_CHECK_LAUNCH();
       return TW_OK;
     }
