@@ -517,16 +517,18 @@ struct GemvKV {
   const int* t;
 };
 
-template <int MR, int CPW>
+template <int MR, int CPW, int PRE>
 __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                    float eps, GemvKV kv) {
   extern __shared__ __attribute__((aligned(16))) char gemv_smem[];
   bf16* xs = (bf16*)gemv_smem;                         // [MR][K] bf16
   const int lane = lane_id(), wave = wave_id_uniform();
   const int K = p.K;
-  // this wave's W rows (CPW output columns): the first (up to) GV_PRE 16-B pieces per lane are loaded
-  // before the A rows are staged, so their HBM latency hides behind the LayerNorm / LDS prologue
-  constexpr int GV_PRE = CPW == 1 ? 12 : 3;
+  // this wave's W rows (CPW output columns): the first (up to) PRE 16-B pieces per lane are loaded before
+  // the A rows are staged, so their HBM latency hides behind the LayerNorm / LDS prologue.  PRE is sized to
+  // K (3 pieces cover K = 1280, 10 cover 5120): more registers would cut the waves per SIMD, and the
+  // 1280-workgroup fc1 GEMV needs 5 per SIMD to run in one round (measured: 9.6 -> 13.8 us at PRE = 12)
+  constexpr int GV_PRE = PRE;
   const int n0 = (blockIdx.x * 4 + wave) * CPW;
   bf16x8 wpre[CPW][GV_PRE];
   const int npre = min(GV_PRE, (K - lane * 8 + 511) / 512);
@@ -930,15 +932,20 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
   const int cpw = N >= 16384 ? 8 : 1;
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
   const size_t lds = (size_t)(M == 1 ? 1 : M == 2 ? 2 : 4) * K * 2;
-#define TW_GEMV(MR_, CPW_) hipLaunchKernelGGL((gemv_kernel<MR_, CPW_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
+#define TW_GEMV(MR_, CPW_, PRE_) \
+  hipLaunchKernelGGL((gemv_kernel<MR_, CPW_, PRE_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
   if (cpw == 8) {
-    if (M == 1) TW_GEMV(1, 8);
-    else if (M == 2) TW_GEMV(2, 8);
-    else TW_GEMV(4, 8);
+    if (M == 1) TW_GEMV(1, 8, 3);
+    else if (M == 2) TW_GEMV(2, 8, 3);
+    else TW_GEMV(4, 8, 3);
+  } else if (K <= 1536) {
+    if (M == 1) TW_GEMV(1, 1, 3);
+    else if (M == 2) TW_GEMV(2, 1, 3);
+    else TW_GEMV(4, 1, 3);
   } else {
-    if (M == 1) TW_GEMV(1, 1);
-    else if (M == 2) TW_GEMV(2, 1);
-    else TW_GEMV(4, 1);
+    if (M == 1) TW_GEMV(1, 1, 10);
+    else if (M == 2) TW_GEMV(2, 1, 10);
+    else TW_GEMV(4, 1, 10);
   }
 #undef TW_GEMV
   TW_CHECK_LAUNCH();
