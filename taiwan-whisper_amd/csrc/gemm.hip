@@ -497,6 +497,25 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmP p, int S) {
   }
 }
 
+// the same, 4 consecutive columns per thread (N % 4 == 0, ldc / ws rows 16-B aligned): the split-K tail
+// of the mid-sized forward GEMMs
+__global__ __launch_bounds__(256) void sk_reduce_kernel(GemmP p, int S) {
+  const int n4 = p.N >> 2;
+  const int64_t total = (int64_t)p.M * p.N, work = (int64_t)p.M * n4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < work; i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
+    const float* w = p.ws + (int64_t)m * p.N + n;
+    f32x4 a = *(const f32x4*)w;
+    for (int s = 1; s < S; ++s) a += *(const f32x4*)(w + s * total);
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = epi_value(p, m, n + r, a[r]);
+    const int64_t co = (int64_t)m * p.ldc + n;
+    if (p.c_dtype == TW_BF16) *(bf16x4*)((bf16*)p.C + co) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    else *(f32x4*)((float*)p.C + co) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // GEMV for the batch-1 (and up to 4-row) decode step: one output column per wave, 4 per workgroup
 // (N / 4 workgroups: 320 for N = 1280, where the 16-column skinny kernel has 80).  The A rows go to LDS
@@ -792,7 +811,78 @@ void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
   if (tile == 2562 && !AT && !BT) launch_pp(p, batch, stream);
   else if (tile == 256) launch<AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
   else if (tile == 2561) launch<AT, BT, 256, 128, 4, 2, 3>(p, batch, stream);
+  else if (tile == 2563) launch<AT, BT, 256, 128, 4, 2, 2>(p, batch, stream);
   else launch<AT, BT, 128, 128, 2, 2, 2>(p, batch, stream);
+}
+
+int pp_grid_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n >= 8 ? n : 8;
+  }();
+  return cus & ~7;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Data-parallel + split-K tail for the mid-sized forward GEMMs (the decoder's N = 1280 Linears at
+// M = 64 x 447: 560 256-tiles = 2.19 rounds of the 256 persistent workgroups).  The m-tile rows that
+// fill whole rounds run as ordinary persistent tiles (full epilogue); the remaining m-tile rows are cut
+// into S equal K chunks run as S batch entries of the same kernel into fp32 partials (one round),
+// then skinny_reduce_kernel sums the chunks in order and applies the full epilogue to those rows.
+// Returns S (0 = no plan: the caller takes the 128x128 path).  Numerics: the tail rows' fp32 sum over
+// K is regrouped by chunk (as the dW split-K); every other row is the unsplit kernel's.
+// ---------------------------------------------------------------------------------------------
+int sk_tail_plan(const GemmP& p, int batch, int& m_dp) {
+  if (batch != 1 || p.res_mod != 0 || (p.N & 3) || (p.ldc & 3) || ((uintptr_t)p.C & 15)) return 0;
+  const int G = pp_grid_cus();
+  const int tn = (p.N + 255) / 256, tm = (p.M + 255) / 256;
+  const int64_t T = (int64_t)tn * tm;
+  if (T < G || T >= 4 * G) return 0;                  // < 1 round: nothing to fill; many rounds: tail small
+  m_dp = (int)((T / G) * G / tn);                      // m-tile rows of whole rounds
+  const int tail = (tm - m_dp) * tn;
+  if (tail <= 0 || m_dp <= 0) return 0;
+  int best = 0;
+  for (int S = 2; S <= 8; ++S)
+    if (p.K % (64 * S) == 0 && (int64_t)tail * S <= G && p.K / S >= 256) best = S;
+  return best;
+}
+
+int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
+  const int Mt = p.M - m_dp * 256;
+  const size_t bytes = (size_t)S * Mt * p.N * sizeof(float);
+  float* ws = (float*)splitk_workspace(stream, bytes);
+  if (!ws) return 0;
+  GemmP d = p;                                         // whole rounds: the unsplit kernel
+  d.M = m_dp * 256;
+  launch_pp(d, 1, stream);
+  TW_CHECK_LAUNCH();
+  GemmP q = p;                                         // tail rows: S K-chunks -> fp32 partials
+  const int64_t r0 = (int64_t)m_dp * 256;
+  q.A = p.A + r0 * p.lda;
+  q.M = Mt;
+  q.K = p.K / S;
+  q.sA = q.K;                                          // chunk s starts at column s*K/S of A and B
+  q.sB = q.K;
+  q.C = ws; q.ldc = p.N; q.sC = (int64_t)Mt * p.N; q.c_dtype = TW_F32;
+  q.alpha = 1.f; q.flags = 0; q.bias = nullptr; q.res = nullptr; q.aux = nullptr; q.ws = nullptr;
+  q.group_m = 1;
+  q.epi = pick_epilogue(q, S);
+  launch_pp(q, S, stream);
+  TW_CHECK_LAUNCH();
+  GemmP r = p;                                         // ordered chunk sum + the full epilogue
+  const int csz = p.c_dtype == TW_BF16 ? 2 : 4;
+  r.C = (char*)p.C + r0 * p.ldc * csz;
+  if (p.res) r.res = (const char*)p.res + r0 * p.ldr * (p.res_dtype == TW_BF16 ? 2 : 4);
+  if (p.aux) r.aux = p.aux + r0 * p.ldaux;
+  r.M = Mt;
+  r.ws = ws;
+  const int64_t work = (int64_t)Mt * (p.N / 4);
+  hipLaunchKernelGGL(sk_reduce_kernel, dim3((int)std::min<int64_t>((work + 255) / 256, 4096)), dim3(256), 0,
+                     stream, r, S);
+  TW_CHECK_LAUNCH();
+  return 1;
 }
 
 }  // namespace
@@ -897,6 +987,21 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
       TW_CHECK_LAUNCH();
       return TW_OK;
     }
+  }
+  // mid-sized forward grids (1-4 rounds of 256-tiles): whole rounds persistent + a split-K tail
+  // (TW_GEMM_SK=0 disables it for A/B runs; flag 262144 forces the 256x128 2-stage tile)
+  static const int env_sk = [] {
+    const char* e = getenv("TW_GEMM_SK");
+    return e ? atoi(e) : 1;
+  }();
+  if (flags & 262144) tile = 2563;
+  // (tools/bench_gemm_dec.py: fc2 K = 5120 417 -> 347 us; at K = 1280 the split's fp32 round trip costs
+  // more than the third round it saves, 125 -> 140 us, so short K stays on the 128x128 kernel)
+  if (!a_trans && !b_trans && tile == 128 && env_sk && K >= 3072 &&
+      !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
+    int m_dp = 0;
+    const int S = sk_tail_plan(p, batch, m_dp);
+    if (S > 0 && launch_sk_tail(p, S, m_dp, stream)) return TW_OK;
   }
   if (!a_trans && !b_trans) dispatch<false, false>(p, batch, stream, tile);
   else if (!a_trans && b_trans) dispatch<false, true>(p, batch, stream, tile);

@@ -2,7 +2,7 @@ import os, sys
 sys.path.insert(0, "taiwan-whisper_amd")
 import torch
 from tw import ops
-V = (("t128", 256), ("t256", 512), ("s3", 1024), ("pp", 2048))
+V = (("t128", 256), ("s2", 262144), ("pp", 2048), ("dflt", 0))
 for name, M, N, K, flags in (("dec out", 28608, 1280, 1280, 0), ("dec fc2", 28608, 1280, 5120, 0),
                              ("dec out res", 28608, 1280, 1280, 1), ("dec fc2 res", 28608, 1280, 5120, 1),
                              ("dec q", 28608, 1280, 1280, 2), ("enc out res", 96000, 1280, 1280, 1),

@@ -291,6 +291,65 @@ def test_gemm_pp_grouped_tile_order():
     assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
 
 
+@pytest.mark.parametrize("M,N,K", [(28608, 1280, 5120), (11000, 1288, 4096)])
+def test_gemm_sk_tail_forward(M, N, K):
+    """Mid-sized long-K forward GEMMs (1-4 rounds of 256-tiles, K >= 3072: the decoder's fc2 at B = 64) take
+    whole rounds on the persistent kernel and the remaining m-tile rows as split-K chunks + an ordered
+    fp32 reduce with the full epilogue.  Rows of the whole rounds equal the 128x128 kernel bit for bit
+    (same K order); the tail rows regroup the fp32 sum by chunk, so they may sit one bf16 ulp away (the
+    rounding boundary) — checked against the 128x128 kernel and fp64 on sampled rows.  Epilogues: bias +
+    round, bias + round + GELU with the pre-activation aux, in-place bf16 residual."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    res0 = bf(torch.randn(M, N, generator=g)).to(DEV)
+    outs = {}
+    for name, f in (("t128", ops.GEMM_TILE128), ("sk", 0)):
+        o = {}
+        C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, flags=ops.GEMM_ROUND | f)
+        o["bf16"] = C
+        Cg = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        aux = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, Cg, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, aux=aux, ldaux=N,
+                 flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT | f)
+        o["gelu"], o["aux"] = Cg, aux
+        rb = res0.clone()
+        ops.gemm(Ad, Wd, rb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rb, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_bf16"] = rb
+        outs[name] = o
+    torch.cuda.synchronize()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count & ~7
+    tn, tm = (N + 255) // 256, (M + 255) // 256
+    m_dp = (tn * tm // cus) * cus // tn * 256                # rows of the whole rounds
+    assert 0 < m_dp < M
+    same_pre = outs["sk"]["aux"][m_dp:] == outs["t128"]["aux"][m_dp:]
+    for kind in ("bf16", "gelu", "aux", "res_bf16"):
+        got, ref = outs["sk"][kind], outs["t128"][kind]
+        assert not torch.isnan(got).any(), kind
+        assert torch.equal(got[:m_dp], ref[:m_dp]), kind
+        d = (got[m_dp:].float() - ref[m_dp:].float()).abs()
+        # adjacent bf16 values, plus the fp32 regrouping term on cancellation (acc + bias ~ 0): 2e-6 of the
+        # largest value (the f32 sums differ by ~1e-7 relative)
+        tol = torch.maximum(ref[m_dp:].float().abs(), got[m_dp:].float().abs()) * 2 ** -7 \
+            + 2e-6 * float(ref.float().abs().max())
+        if kind == "gelu":      # equal pre-activation -> equal GELU; a flipped one moves it by <= max|gelu'| ulp
+            assert bool((d[same_pre] == 0).all())
+            pre = torch.maximum(outs["sk"]["aux"][m_dp:].float().abs(), outs["t128"]["aux"][m_dp:].float().abs())
+            tol = tol + 1.13 * pre * 2 ** -7
+        if kind == "res_bf16":  # bf16(y) + res: a flipped y moves the sum by one ulp of y
+            y = torch.maximum(outs["sk"]["bf16"][m_dp:].float().abs(), outs["t128"]["bf16"][m_dp:].float().abs())
+            tol = tol + y * 2 ** -7
+        assert bool((d <= tol).all()), (kind, float((d - tol).max()))
+        assert float((d > 0).float().mean()) < 0.02, kind    # rounding-boundary cases only
+    rows = torch.tensor([0, m_dp - 1, m_dp, (m_dp + M) // 2, M - 1])
+    ref = bf((bf(A[rows]).double() @ bf(W).double().T + bf(bias).double()).float()).float()
+    got = outs["sk"]["bf16"][rows.to(DEV)].float().cpu()
+    assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
+
+
 @pytest.mark.parametrize("N,K,M", [(1280, 1280, 28608), (2560, 1280, 8192), (264, 136, 4096), (1280, 1280, 1000)])
 def test_gemm_splitk_weight_grad(N, K, M):
     """dW[N][K] += round(dY^T X) with dY [M][N], X [M][K] (both MN-major operands, fp32 accumulate): the
