@@ -8,11 +8,17 @@ namespace {
 
 constexpr int WPB = 4;   // waves (rows) per block
 
-template <int VEC, int MAXJ>
+// ADD (fp32 x, VEC 4 only): the residual update of the preceding Linear fused in front of the
+// statistics -- x_out = x + r (r = the Linear's bf16 output, the same fp32 add the GEMM's residual
+// epilogue performs, so x_out is bit-identical), then the LayerNorm of x_out.  This moves the fp32
+// residual read + write out of the GEMM epilogue, where every CU of the persistent kernel issues it
+// at once between two tiles, into this streaming pass.
+template <int VEC, int MAXJ, bool ADD = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_dtype,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      void* __restrict__ y, int y_dtype, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out, int rows, int D, float eps) {
+                                                     float* __restrict__ rstd_out, int rows, int D, float eps,
+                                                     const bf16* __restrict__ r = nullptr, float* x_out = nullptr) {
   const int lane = lane_id();
   const int row = blockIdx.x * WPB + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -24,7 +30,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
   for (int j = 0; j < MAXJ; ++j) {
     if (j < J) {
       const int e = (j * 64 + lane) * VEC;
-      if (VEC == 4) {
+      if constexpr (ADD) {
+        const f32x4 t = *(const f32x4*)((const float*)x + base + e);
+        const bf16x4 u = *(const bf16x4*)(r + base + e);
+        const f32x4 o = f32x4{t[0] + bf2f(u[0]), t[1] + bf2f(u[1]), t[2] + bf2f(u[2]), t[3] + bf2f(u[3])};
+        *(f32x4*)(x_out + base + e) = o;
+        v[j][0] = o[0]; v[j][1] = o[1]; v[j][2] = o[2]; v[j][3] = o[3];
+      } else if (VEC == 4) {
         if (x_dtype == TW_F32) {
           f32x4 t = *(const f32x4*)((const float*)x + base + e);
           v[j][0] = t[0]; v[j][1] = t[1]; v[j][2] = t[2]; v[j][3] = t[3];
@@ -249,6 +261,19 @@ extern "C" int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, cons
   else
     hipLaunchKernelGGL((ln_fwd_kernel<1, 20>), grid, block, 0, stream, x, x_dtype, w, b, y, y_dtype, mean_out,
                        rstd_out, rows, D, eps);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_add_layernorm_fwd(const float* x, const void* r, float* x_out, const float* w, const float* b,
+                                    void* y, float* mean_out, float* rstd_out, int rows, int D, float eps,
+                                    hipStream_t stream) {
+  if (rows <= 0) return TW_OK;
+  if (D % 256 || D > 1280) return TW_EUNSUPPORTED;
+  if ((((uintptr_t)x | (uintptr_t)r | (uintptr_t)x_out | (uintptr_t)y) & 15) != 0) return TW_EINVAL;
+  hipLaunchKernelGGL((ln_fwd_kernel<4, 5, true>), dim3((rows + WPB - 1) / WPB), dim3(64 * WPB), 0, stream,
+                     (const void*)x, (int)TW_F32, w, b, y, (int)TW_BF16, mean_out, rstd_out, rows, D, eps,
+                     (const bf16*)r, x_out);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -24,6 +24,8 @@ def t(fn, rounds=5, reps=3):
 
 
 VARIANTS = (("t256", ops.GEMM_TILE256), ("s3", ops.GEMM_TILE256x128), ("pp", ops.GEMM_TILE256PP))
+if os.environ.get("PP_ONLY"):
+    VARIANTS = (("pp", ops.GEMM_TILE256PP),)
 
 
 def main():

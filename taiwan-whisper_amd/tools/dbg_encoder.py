@@ -69,9 +69,13 @@ def main():
     xcur = xs
     for i in range(cfg["encoder_layers"]):
         pf = f"model.encoder.layers.{i}"
-        xcur = s._attn_block(xcur, pf + ".self_attn", B, T, False)
+        xcur, pend = s._attn_block(xcur, pf + ".self_attn", B, T, False)
+        if pend is not None:                 # deferred residual update: apply it for the stage dump
+            xcur = xcur + pend.float()
         hs.append((f"layer {i} attn", xcur.view(B, T, d).clone()))
-        xcur = s._mlp_block(xcur, pf)
+        xcur, pend = s._mlp_block(xcur, pf)
+        if pend is not None:
+            xcur = xcur + pend.float()
         hs.append((f"layer {i} mlp", xcur.view(B, T, d).clone()))
     for (n, a), (_, b) in zip(hs, stages_ref):
         print(f"{n:14s} rel-L2 {rl2(a, b):.3e}")

@@ -34,6 +34,8 @@ import torch
 from . import ops
 from .config import GenerationConfig, WhisperConfig
 
+_DEFER_RES = os.environ.get("TW_DEFER_RES", "1") != "0"
+
 F = ops
 
 
@@ -434,12 +436,48 @@ class WhisperForConditionalGeneration:
         F.layernorm_fwd(x, self.ln_param(name + ".weight"), self.ln_param(name + ".bias"), y, mean, rstd)
         return y
 
-    def _attn_block(self, x, p, B, T, causal, tape=None):
-        """x: residual stream [B*T, d] -> new residual stream (self attention)."""
+    @property
+    def defer_residual(self):
+        """fp32 residual stream under autocast (the student): the stream-updating Linears (out_proj, fc2)
+        write their bf16 output and the next LayerNorm adds it to the stream (tw_add_layernorm_fwd, the same
+        fp32 add): the fp32 read-modify-write leaves the persistent GEMM's epilogue.
+        TW_DEFER_RES=0 keeps it in the epilogue (A/B runs)."""
+        return (self.stream_dtype == torch.float32 and self.act_dtype == torch.bfloat16
+                and self.config.d_model % 256 == 0 and _DEFER_RES)
+
+    def _ln_in(self, x, pend, name, save):
+        """Block-entry LayerNorm -> (stream, LN output).  pend: a deferred residual update (bf16), added to
+        the stream first (in place, or into a fresh buffer when a tape holds the old stream)."""
+        if pend is None:
+            return x, self._ln(x, name, save=save)
+        xn = x if save is None else torch.empty_like(x)
+        y = torch.empty(x.shape, dtype=self.act_dtype, device=self.device)
+        mean = rstd = None
+        if save is not None:
+            mean = torch.empty(x.shape[0], dtype=torch.float32, device=self.device)
+            rstd = torch.empty_like(mean)
+            save[name] = (xn, mean, rstd, y)
+        F.add_layernorm_fwd(x, pend, xn, self.ln_param(name + ".weight"), self.ln_param(name + ".bias"), y, mean, rstd)
+        return xn, y
+
+    def _res_out(self, h, w, b, x, tape):
+        """The stream-updating Linear -> (stream, pending update): deferred to the next LayerNorm on fp32
+        streams, else applied by the GEMM's residual epilogue."""
+        M, N = h.shape[0], w.shape[0]
+        if self.defer_residual:
+            r = torch.empty(M, N, dtype=self.act_dtype, device=self.device)
+            self._lin(h, w, b, r)
+            return x, r
+        out = torch.empty(M, N, dtype=self.stream_dtype, device=self.device) if tape is not None else x
+        self._lin(h, w, b, out, res=x)
+        return out, None
+
+    def _attn_block(self, x, p, B, T, causal, tape=None, pend=None):
+        """x: residual stream [B*T, d] (+ a pending update) -> (new stream, pending update) (self attention)."""
         cfg, d = self.config, self.config.d_model
         H = d // 64
         sv = {} if tape is not None else None
-        y = self._ln(x, p + "_layer_norm", save=sv)
+        x, y = self._ln_in(x, pend, p + "_layer_norm", sv)
         M = B * T
         qkv = torch.empty(M, 3 * d, dtype=self.act_dtype, device=self.device)
         wqkv = self.wspan(p + ".q_proj.weight", p + ".v_proj.weight", (3 * d, d))
@@ -448,18 +486,16 @@ class WhisperForConditionalGeneration:
         o = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         lse = torch.empty(B * H * T, dtype=torch.float32, device=self.device) if tape is not None else None
         F.attn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, o, d, lse, B, H, T, T, causal, 0.125)
-        out = torch.empty(M, d, dtype=self.stream_dtype, device=self.device) if tape is not None else x
-        self._lin(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), out, res=x,
-                  flags=F.GEMM_ROUND)
+        out = self._res_out(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), x, tape)
         if tape is not None:
             tape.append(("attn", p, dict(sv=sv, y=y, qkv=qkv, o=o, lse=lse, B=B, T=T, causal=causal)))
         return out
 
-    def _cross_block(self, x, enc16, p, B, T, Tk, tape=None, kv=None):
+    def _cross_block(self, x, enc16, p, B, T, Tk, tape=None, kv=None, pend=None):
         d = self.config.d_model
         H = d // 64
         sv = {} if tape is not None else None
-        y = self._ln(x, p + "_layer_norm", save=sv)
+        x, y = self._ln_in(x, pend, p + "_layer_norm", sv)
         M = B * T
         q = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         self._lin(y, self._w16(p + ".q_proj.weight"), self._w16(p + ".q_proj.bias"), q)
@@ -471,24 +507,21 @@ class WhisperForConditionalGeneration:
         o = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         lse = torch.empty(B * H * T, dtype=torch.float32, device=self.device) if tape is not None else None
         F.attn_fwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, o, d, lse, B, H, T, Tk, False, 0.125)
-        out = torch.empty(M, d, dtype=self.stream_dtype, device=self.device) if tape is not None else x
-        self._lin(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), out, res=x)
+        out = self._res_out(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), x, tape)
         if tape is not None:
             tape.append(("cross", p, dict(sv=sv, y=y, q=q, kv=kv, o=o, lse=lse, B=B, T=T, Tk=Tk)))
         return out
 
-    def _mlp_block(self, x, p, tape=None):
+    def _mlp_block(self, x, p, tape=None, pend=None):
         M = x.shape[0]
         sv = {} if tape is not None else None
-        y = self._ln(x, p + ".final_layer_norm", save=sv)
+        x, y = self._ln_in(x, pend, p + ".final_layer_norm", sv)
         f = self.store.segs[p + ".fc1.weight"][0]
         h = torch.empty(M, f, dtype=self.act_dtype, device=self.device)
         pre = torch.empty(M, f, dtype=self.act_dtype, device=self.device) if tape is not None else None
         self._lin(y, self._w16(p + ".fc1.weight"), self._w16(p + ".fc1.bias"), h, aux=pre,
                   flags=F.GEMM_ROUND | F.GEMM_GELU | (F.GEMM_AUX_OUT if tape is not None else 0))
-        out = torch.empty(M, self.config.d_model, dtype=self.stream_dtype, device=self.device) \
-            if tape is not None else x
-        self._lin(h, self._w16(p + ".fc2.weight"), self._w16(p + ".fc2.bias"), out, res=x)
+        out = self._res_out(h, self._w16(p + ".fc2.weight"), self._w16(p + ".fc2.bias"), x, tape)
         if tape is not None:
             tape.append(("mlp", p, dict(sv=sv, y=y, h=h, pre=pre)))
         return out
@@ -532,12 +565,13 @@ class WhisperForConditionalGeneration:
                aux=pre2, ldaux=d, sAux=T * d, flags=gf)
         if tape is not None:
             tape.append(("conv", "model.encoder", dict(conv_in=conv_in, H1=H1, pre1=pre1, pre2=pre2, B=B, T=T)))
+        pend = None
         for i in range(cfg.encoder_layers):
             p = f"model.encoder.layers.{i}"
-            x = self._attn_block(x, p + ".self_attn", B, T, False, tape)
-            x = self._mlp_block(x, p, tape)
+            x, pend = self._attn_block(x, p + ".self_attn", B, T, False, tape, pend)
+            x, pend = self._mlp_block(x, p, tape, pend)
         sv = {} if tape is not None else None
-        enc = self._ln(x, "model.encoder.layer_norm", save=sv)
+        _, enc = self._ln_in(x, pend, "model.encoder.layer_norm", sv)
         if tape is not None:
             tape.append(("ln_final", "model.encoder.layer_norm", dict(sv=sv)))
         return enc
@@ -564,13 +598,14 @@ class WhisperForConditionalGeneration:
         x = self.embed(ids)
         if tape is not None:
             tape.append(("embed", "model.decoder", dict(ids=ids.reshape(-1).contiguous(), B=B, T=T)))
+        pend = None
         for i in range(cfg.decoder_layers):
             p = f"model.decoder.layers.{i}"
-            x = self._attn_block(x, p + ".self_attn", B, T, True, tape)
-            x = self._cross_block(x, enc16, p + ".encoder_attn", B, T, Tk, tape)
-            x = self._mlp_block(x, p, tape)
+            x, pend = self._attn_block(x, p + ".self_attn", B, T, True, tape, pend)
+            x, pend = self._cross_block(x, enc16, p + ".encoder_attn", B, T, Tk, tape, pend=pend)
+            x, pend = self._mlp_block(x, p, tape, pend)
         sv = {} if tape is not None else None
-        h = self._ln(x, "model.decoder.layer_norm", save=sv)
+        _, h = self._ln_in(x, pend, "model.decoder.layer_norm", sv)
         if tape is not None:
             tape.append(("ln_final", "model.decoder.layer_norm", dict(sv=sv)))
         return h

@@ -461,6 +461,39 @@ def test_layernorm(D, xdt):
     assert rel_err(dw, wr.grad) < 1e-4 and rel_err(db, br.grad) < 1e-4
 
 
+@pytest.mark.parametrize("D", [768, 1280])
+def test_add_layernorm_matches_residual_epilogue(D):
+    """Deferred residual update (fp32 stream): the Linear's bf16 output r added by the next LayerNorm
+    (tw_add_layernorm_fwd) == the GEMM's residual epilogue followed by tw_layernorm_fwd, bit for bit,
+    in place and into a separate stream buffer."""
+    from tw import ops
+    g = torch.Generator().manual_seed(D + 1)
+    rows, K = 1000, 256
+    x0 = (torch.randn(rows, D, generator=g) * 3).to(DEV)
+    A, W = bf(torch.randn(rows, K, generator=g)).to(DEV), bf(torch.randn(D, K, generator=g) * 0.1).to(DEV)
+    bias = bf(torch.randn(D, generator=g)).to(DEV)
+    w, b = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    # reference: residual epilogue in the GEMM, then the plain LayerNorm
+    xa = x0.clone()
+    ops.gemm(A, W, xa, rows, D, K, lda=K, ldb=K, ldc=D, bias=bias, res=xa, ldr=D, flags=ops.GEMM_ROUND)
+    ya = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    ma, ra = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(xa, w, b, ya, ma, ra)
+    # deferred: bf16 Linear output, then add + LayerNorm
+    r = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(A, W, r, rows, D, K, lda=K, ldb=K, ldc=D, bias=bias, flags=ops.GEMM_ROUND)
+    for inplace in (True, False):
+        xb = x0.clone()
+        xo = xb if inplace else torch.empty_like(xb)
+        yb = torch.empty_like(ya)
+        mb, rb = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+        ops.add_layernorm_fwd(xb, r, xo, w, b, yb, mb, rb)
+        torch.cuda.synchronize()
+        assert torch.equal(xo, xa) and torch.equal(yb, ya) and torch.equal(mb, ma) and torch.equal(rb, ra)
+        if not inplace:
+            assert torch.equal(xb, x0)
+
+
 # ----------------------------------------------------------------------------- attention
 def ref_attn(q, k, v, causal, scale):
     s = (q.double() @ k.double().transpose(-1, -2)) * scale
