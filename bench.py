@@ -337,7 +337,7 @@ def main():
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    timer = KernelTimer("gemm_nn")
+    timer = KernelTimer("gemm_nn", "gemm_nn_lt")
     with timer:
         t0 = time.perf_counter()
         for i in range(args.steps):
@@ -353,6 +353,7 @@ def main():
     elapsed = float(elapsed.item())
     loss = float(m["loss"].item())
     ks = timer.summary()
+    ks_lt = timer.summary("gemm_nn_lt")
 
     teacher_ms = None
     if not args.no_teacher_fwd:
@@ -383,11 +384,20 @@ def main():
                         frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=pmc,
                         mfma_busy_frac=(load_mfma("c3_step", "gemm_pp (persistent 256x256 forward GEMM)")
                                         if args.config == "c3" else None),
-                        kernel="tw_gemm_bf16 K-major x K-major launches (every forward X.W^T of the step): "
-                               "gemm_pp_kernel (persistent 256x256 ping-pong) + gemm_kernel<false,false,128,...> "
-                               "for grids under ~1000 256-tiles",
+                        kernel="hand-written tw_gemm_bf16 K-major x K-major launches (the forward X.W^T with fused "
+                               "epilogues: GELU fc1, residual out_proj/fc2 of bf16 streams, long-K fc2): "
+                               "gemm_pp_kernel (persistent 256x256 ping-pong, + split-K tail) + "
+                               "gemm_kernel<false,false,128,...> for grids under ~1000 256-tiles",
                         launches_per_step=ks["launches"] // args.steps, avg_launch_ms=round(ks["avg_ms"], 4),
                         algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4))
+        vendor = None
+        if ks_lt is not None:      # the plain-bias projections routed to hipBLASLt (tw_gemm_backend == 1)
+            vendor = dict(launches_per_step=ks_lt["launches"] // args.steps,
+                          achieved_tflops=round(ks_lt["rate"] / 1e12, 2),
+                          frac=round(ks_lt["rate"] / 1e12 / PEAK_BF16_TFLOPS, 4),
+                          ms_per_step=round(ks_lt["total_ms"] / args.steps, 2),
+                          kernel="hipBLASLt (TN, bias epilogue, bf16 out): QKV / cross-KV / cross-Q / out_proj of fp32 streams (residual "
+                                 "deferred to the next LN) / tied LM head, K <= 2048")
         out = {
             "metric": "distillation utterances/sec (30 s clips)",
             "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
@@ -409,6 +419,7 @@ def main():
             "step_mfma_frac": round(flops_clip * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(loss, 4),
             "roofline": roof,
+            "vendor_gemm": vendor,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -38,6 +38,11 @@ typedef void* tw_stream_t; /* hipStream_t */
 #define TW_GEMM_TILE256x128 1024  /* force the 256x128 tile with the 3-stage LDS ring */
 #define TW_GEMM_TILE256PP 2048    /* force the 256x256 ping-pong kernel (a_trans = b_trans = 0 only) */
 
+/* Backend tw_gemm_bf16 takes for a call of this shape: 0 = the hand-written kernels (gemm.hip), 1 = hipBLASLt
+ * for the plain forward projections (K-major operands, bf16 output, bias / round only, alpha 1, K <= 2048,
+ * M >= 4096, N >= 256; csrc/gemm_vendor.hip).  Lets a caller attribute timings; TW_GEMM_VENDOR=0 disables. */
+int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, int c_dtype, int batch, float alpha, int flags);
+
 /* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
  * Replaces every nn.Linear / Conv1d (as GEMM) / tied proj_out matmul of the step, forward and
  * backward: HF modeling_whisper.py:279-345 (q/k/v/out_proj), :618-619 (conv1/conv2), :400-410 and

@@ -887,8 +887,25 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
 
 }  // namespace
 
+int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
+                        int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream);
+
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
 void* tw_device_workspace(hipStream_t stream, size_t bytes) { return splitk_workspace(stream, bytes); }
+
+// Which implementation tw_gemm_bf16 runs for a call of this shape: 0 = the kernels of this file, 1 = hipBLASLt
+// (plain forward projections: K-major operands, bf16 output, bias/round only, alpha 1, K <= 2048, M >= 4096,
+// N >= 256, no forced tile).  TW_GEMM_VENDOR=0 keeps everything on the own kernels (A/B runs).
+extern "C" int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, int c_dtype, int batch, float alpha,
+                               int flags) {
+  static const int env_vendor = [] {
+    const char* e = getenv("TW_GEMM_VENDOR");
+    return e ? atoi(e) : 1;
+  }();
+  return (env_vendor && !a_trans && !b_trans && batch == 1 && c_dtype == TW_BF16 && alpha == 1.f &&
+          (flags & 0xff & ~(F_BIAS | F_ROUND)) == 0 && K <= 2048 && M >= 4096 && N >= 256 &&
+          !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) ? 1 : 0;
+}
 
 extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
                             void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
@@ -986,6 +1003,17 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
                          (flags & F_ACCUM) ? 1 : 0);
       TW_CHECK_LAUNCH();
       return TW_OK;
+    }
+  }
+  // plain forward projections (bias + bf16 out, K <= 2048, M >= 4096): hipBLASLt (csrc/gemm_vendor.hip)
+  if (tw_gemm_backend(M, N, K, a_trans, b_trans, c_dtype, batch, alpha, flags) == 1) {
+    const size_t ws_bytes = (size_t)64 << 20;
+    void* ws = splitk_workspace(stream, ws_bytes);
+    if (ws) {
+      const int r = tw_vendor_gemm_bf16(A, lda, B, ldb, C, ldc, M, N, K, (flags & F_BIAS) ? bias : nullptr, ws,
+                                        ws_bytes, stream);
+      if (r == 1) return TW_OK;
+      if (r < 0) return TW_EHIP;
     }
   }
   // mid-sized forward grids (1-4 rounds of 256-tiles): whole rounds persistent + a split-K tail

@@ -16,6 +16,7 @@ P, I64, I32, F32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 
 # name -> argtypes (return type is always int status)
 SIGNATURES = {
+    "tw_gemm_backend": [I32, I32, I32, I32, I32, I32, I32, F32, I32],
     "tw_gemm_bf16": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I32, I64, I64, I64, F32, P,
                      P, I64, I64, I32, I32, P, I64, I64, I32, P],
     "tw_flac_info": [P, I64, P],
@@ -82,6 +83,11 @@ def lib():
             f.restype = ctypes.c_int
         _lib = l
     return _lib
+
+
+def query(name: str, *args) -> int:
+    """A C-ABI entry whose int return is a value, not a status (tw_gemm_backend)."""
+    return int(getattr(lib(), name)(*args))
 
 
 def call(name: str, *args):

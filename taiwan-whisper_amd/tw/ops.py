@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from ._native import call
+from ._native import call, query
 from .profiling import KernelTimer
 
 F32, BF16 = 0, 1
@@ -75,6 +75,9 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
         assert aux.dtype == torch.bfloat16
         _need(aux, (batch - 1) * sAux + (M - 1) * ldaux + N, "gemm aux")
     fam = "gemm_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
+    if KernelTimer.active is not None and query("tw_gemm_backend", M, N, K, int(a_trans), int(b_trans), _dt(C),
+                                                 batch, float(alpha), flags) == 1:
+        fam += "_lt"                 # timed apart: this call runs on hipBLASLt (include/tw_hip.h tw_gemm_backend)
     flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
     KernelTimer.wrap(fam, flops, lambda: call(
         "tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),

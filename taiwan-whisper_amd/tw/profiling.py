@@ -9,9 +9,10 @@ import torch
 class KernelTimer:
     active = None   # the KernelTimer currently collecting, or None
 
-    def __init__(self, family: str):
-        self.family = family
-        self.records = []   # (start_event, end_event, algorithmic_flops_or_bytes)
+    def __init__(self, *families: str):
+        self.families = families
+        self.family = families[0]
+        self.records = {f: [] for f in families}   # family -> [(start_event, end_event, algorithmic work)]
 
     def __enter__(self):
         KernelTimer.active = self
@@ -23,19 +24,20 @@ class KernelTimer:
     @staticmethod
     def wrap(family, work, launch):
         t = KernelTimer.active
-        if t is None or t.family != family:
+        if t is None or family not in t.records:
             return launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         r = launch()
         e1.record()
-        t.records.append((e0, e1, work))
+        t.records[family].append((e0, e1, work))
         return r
 
-    def summary(self):
+    def summary(self, family=None):
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b, _ in self.records]
-        work = [w for _, _, w in self.records]
+        rec = self.records[family or self.family]
+        ms = [a.elapsed_time(b) for a, b, _ in rec]
+        work = [w for _, _, w in rec]
         n = len(ms)
         if n == 0:
             return None

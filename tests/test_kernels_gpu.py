@@ -350,6 +350,36 @@ def test_gemm_sk_tail_forward(M, N, K):
     assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
 
 
+@pytest.mark.parametrize("M,N,K,has_bias", [(28608, 3840, 1280, True), (8200, 51904, 1280, False),
+                                             (5000, 1288, 1280, True)])
+def test_gemm_vendor_plain_forward(M, N, K, has_bias):
+    """Plain forward projections (bias + bf16 out, K <= 2048, M >= 4096) run on hipBLASLt: the same
+    autocast arithmetic (fp32 accumulate, + bf16 bias, one bf16 round) as the persistent kernel, so
+    the outputs agree within one bf16 ulp (the fp32 sums may differ in order: plus a cancellation term),
+    sampled rows match fp64 within one ulp, and reruns are bit-identical."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    kw = dict(bias=bd) if has_bias else {}
+    outs = {}
+    for name, f in (("pp", ops.GEMM_TILE256PP), ("vendor", 0), ("vendor2", 0)):
+        C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N, flags=ops.GEMM_ROUND | f, **kw)
+        outs[name] = C
+    torch.cuda.synchronize()
+    got, ref = outs["vendor"].float(), outs["pp"].float()
+    assert not torch.isnan(got).any()
+    assert torch.equal(outs["vendor"], outs["vendor2"])
+    tol = torch.maximum(got.abs(), ref.abs()) * 2 ** -7 + 2e-6 * float(ref.abs().max())
+    assert bool(((got - ref).abs() <= tol).all()), float(((got - ref).abs() - tol).max())
+    rows = torch.tensor([0, M // 3, M - 1])
+    want = bf(A[rows]).double() @ bf(W).double().T + (bf(bias).double() if has_bias else 0)
+    want = bf(want.float()).float()
+    assert (got[rows.to(DEV)].cpu() - want).abs().max() <= 2 ** -7 * want.abs().max()
+
+
 @pytest.mark.parametrize("N,K,M", [(1280, 1280, 28608), (2560, 1280, 8192), (264, 136, 4096), (1280, 1280, 1000)])
 def test_gemm_splitk_weight_grad(N, K, M):
     """dW[N][K] += round(dY^T X) with dY [M][N], X [M][K] (both MN-major operands, fp32 accumulate): the
