@@ -39,8 +39,8 @@ typedef void* tw_stream_t; /* hipStream_t */
 #define TW_GEMM_TILE256PP 2048    /* force the 256x256 ping-pong kernel (a_trans = b_trans = 0 only) */
 
 /* Backend tw_gemm_bf16 takes for a call of this shape: 0 = the hand-written kernels (gemm.hip), 1 = hipBLASLt
- * for the plain forward projections (K-major operands, bf16 output, bias / round only, alpha 1, K <= 2048,
- * M >= 4096, N >= 256; csrc/gemm_vendor.hip).  Lets a caller attribute timings; TW_GEMM_VENDOR=0 disables. */
+ * for the plain projections (K-major A, bf16 output, bias / round only, alpha 1, M >= 4096, N >= 256, and
+ * K <= 2048 with K-major B or K <= 8192 with MN-major B; csrc/gemm_vendor.hip).  Lets a caller attribute timings; TW_GEMM_VENDOR=0 disables. */
 int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, int c_dtype, int batch, float alpha, int flags);
 
 /* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
@@ -120,6 +120,10 @@ int tw_embed_fwd(const int64_t* ids, const void* tok, int tok_dtype, const void*
 int tw_embed_bwd(const int64_t* ids, const float* dh, float* dE, int rows, int D, int64_t padding_idx,
                  tw_stream_t stream);
 
+/* dst[c][r] = src[r][c], bf16 [rows][cols] (row stride ld_src) -> [cols][rows] (ld_dst): the tied
+ * embedding as the K-major operand of the LM-head input gradient (dh = dlogits . E, K = vocabulary). */
+int tw_transpose_bf16(const void* src, int64_t ld_src, int rows, int cols, void* dst, int64_t ld_dst,
+                      tw_stream_t stream);
 /* autocast weight cast fp32 -> bf16 (ACC:accelerator.py autocast of every Linear weight). */
 int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, tw_stream_t stream);
 /* bias gradient: out[c] (+)= [bf16](sum_r x[r][c]); deterministic two-pass, workspace >= ceil(rows/256)*cols. */

@@ -887,8 +887,8 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
 
 }  // namespace
 
-int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
-                        int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream);
+int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int b_trans, void* C, int64_t ldc, int M,
+                        int N, int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream);
 
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
 void* tw_device_workspace(hipStream_t stream, size_t bytes) { return splitk_workspace(stream, bytes); }
@@ -902,8 +902,10 @@ extern "C" int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, in
     const char* e = getenv("TW_GEMM_VENDOR");
     return e ? atoi(e) : 1;
   }();
-  return (env_vendor && !a_trans && !b_trans && batch == 1 && c_dtype == TW_BF16 && alpha == 1.f &&
-          (flags & 0xff & ~(F_BIAS | F_ROUND)) == 0 && K <= 2048 && M >= 4096 && N >= 256 &&
+  // MN-major B (the dX = dY . W products of the backward) up to K = 8192: hipBLASLt's NN kernels measured
+  // 13-30 % faster than the 128x128 kernel (tools/bench_head_bwd.py VENDOR_NN=1)
+  return (env_vendor && !a_trans && batch == 1 && c_dtype == TW_BF16 && alpha == 1.f &&
+          (flags & 0xff & ~(F_BIAS | F_ROUND)) == 0 && K <= (b_trans ? 8192 : 2048) && M >= 4096 && N >= 256 &&
           !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) ? 1 : 0;
 }
 
@@ -948,6 +950,9 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   // 256x256 tile the large transposed ones; 128x128 the small grids (< ~1000 256-tiles).  The
   // 256x128 3-stage ring is kept as a forced variant only.
   int tile = (t256 >= 1000 && K >= 256) ? 256 : 128;
+  // very long K (the LM-head input gradient, K = 51 904): the persistent kernel wins from one round up
+  // (3356 vs 4006 us on 560 tiles, tools/bench_head_bwd.py), its per-tile fixed cost being amortised
+  if (!a_trans && !b_trans && K >= 8192 && t256 >= pp_grid_cus()) tile = 256;
   if (tile == 256 && !a_trans && !b_trans) tile = 2562;
   if (flags & 256) tile = 128;        // forced tile (benchmarking / A-B comparisons)
   if (flags & 512) tile = 256;
@@ -1010,8 +1015,8 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
     const size_t ws_bytes = (size_t)64 << 20;
     void* ws = splitk_workspace(stream, ws_bytes);
     if (ws) {
-      const int r = tw_vendor_gemm_bf16(A, lda, B, ldb, C, ldc, M, N, K, (flags & F_BIAS) ? bias : nullptr, ws,
-                                        ws_bytes, stream);
+      const int r = tw_vendor_gemm_bf16(A, lda, B, ldb, b_trans, C, ldc, M, N, K, (flags & F_BIAS) ? bias : nullptr,
+                                        ws, ws_bytes, stream);
       if (r == 1) return TW_OK;
       if (r < 0) return TW_EHIP;
     }

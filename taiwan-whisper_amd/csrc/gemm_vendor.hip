@@ -27,7 +27,7 @@ struct LtPlan {
   bool ok = false;
 };
 
-using Key = std::tuple<int, int, int, int, int64_t, int64_t, int64_t, int>;   // dev, M, N, K, lda, ldb, ldc, bias
+using Key = std::tuple<int, int, int, int, int64_t, int64_t, int64_t, int, int>;   // dev, M, N, K, lda, ldb, ldc, bias, b_trans
 
 std::mutex g_mu;
 std::map<int, hipblasLtHandle_t> g_handles;
@@ -43,10 +43,10 @@ hipblasLtHandle_t handle_for(int dev) {
 }
 
 bool make_plan(hipblasLtHandle_t h, LtPlan& pl, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
-               bool bias, size_t max_ws) {
+               bool bias, int b_trans, size_t max_ws) {
   if (hipblasLtMatmulDescCreate(&pl.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return false;
   const int32_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
-  hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT));
+  hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSA, b_trans ? &opN : &opT, sizeof(opT));
   hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
   if (bias) {
     const uint32_t epi = HIPBLASLT_EPILOGUE_BIAS;
@@ -54,7 +54,9 @@ bool make_plan(hipblasLtHandle_t h, LtPlan& pl, int M, int N, int K, int64_t lda
     hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
     hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
   }
-  if (hipblasLtMatrixLayoutCreate(&pl.a, HIP_R_16BF, K, N, ldb) != HIPBLAS_STATUS_SUCCESS) return false;   // W
+  // W: [N][K] row-major = column-major K x N (op T); b_trans: [K][N] row-major = column-major N x K (op N)
+  if (hipblasLtMatrixLayoutCreate(&pl.a, HIP_R_16BF, b_trans ? N : K, b_trans ? K : N, ldb) != HIPBLAS_STATUS_SUCCESS)
+    return false;
   if (hipblasLtMatrixLayoutCreate(&pl.b, HIP_R_16BF, K, M, lda) != HIPBLAS_STATUS_SUCCESS) return false;   // X
   if (hipblasLtMatrixLayoutCreate(&pl.d, HIP_R_16BF, N, M, ldc) != HIPBLAS_STATUS_SUCCESS) return false;   // C
   hipblasLtMatmulPreference_t pref = nullptr;
@@ -75,8 +77,8 @@ bool make_plan(hipblasLtHandle_t h, LtPlan& pl, int M, int N, int K, int64_t lda
 
 // 1 = done on hipBLASLt, 0 = not taken (no handle / no algorithm: the caller runs its own kernel),
 // -1 = the launch failed.  `ws` / `ws_bytes`: the per-device stream-ordered scratch block.
-int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
-                        int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream) {
+int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int b_trans, void* C, int64_t ldc, int M,
+                        int N, int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   LtPlan* pl = nullptr;
@@ -85,11 +87,11 @@ int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
     std::lock_guard<std::mutex> lock(g_mu);
     h = handle_for(dev);
     if (!h) return 0;
-    const Key key{dev, M, N, K, lda, ldb, ldc, bias != nullptr};
+    const Key key{dev, M, N, K, lda, ldb, ldc, bias != nullptr, b_trans};
     auto it = g_plans.find(key);
     if (it == g_plans.end()) {
       LtPlan np;
-      np.ok = make_plan(h, np, M, N, K, lda, ldb, ldc, bias != nullptr, ws_bytes);
+      np.ok = make_plan(h, np, M, N, K, lda, ldb, ldc, bias != nullptr, b_trans, ws_bytes);
       it = g_plans.emplace(key, np).first;
     }
     pl = &it->second;

@@ -239,6 +239,49 @@ extern "C" int tw_embed_fwd(const int64_t* ids, const void* tok, int tok_dtype, 
   return TW_OK;
 }
 
+namespace {
+
+// dst[c][r] = src[r][c] for a [rows][cols] bf16 matrix: 64x64 tiles through LDS (16-B row reads, 2-B column
+// writes coalesced per row of the tile; +2 pad per LDS row keeps the transposed reads conflict-light)
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, int64_t lds_, int rows,
+                                                             int cols, bf16* __restrict__ dst, int64_t ldd, int vec) {
+  __shared__ bf16 t[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = tr + 32 * i;
+    if (r0 + r < rows) {
+      if (vec && c0 + tc + 8 <= cols) {
+        const bf16x8 v = *(const bf16x8*)(src + (int64_t)(r0 + r) * lds_ + c0 + tc);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t[r][tc + q] = v[q];
+      } else {
+        for (int q = 0; q < 8; ++q)
+          if (c0 + tc + q < cols) t[r][tc + q] = src[(int64_t)(r0 + r) * lds_ + c0 + tc + q];
+      }
+    }
+  }
+  __syncthreads();
+  const int oc = threadIdx.x & 63, orow = threadIdx.x >> 6;
+  for (int j = orow; j < 64; j += 4) {           // output row c0 + j holds source column c0 + j
+    if (c0 + j < cols && r0 + oc < rows) dst[(int64_t)(c0 + j) * ldd + r0 + oc] = t[oc][j];
+  }
+}
+
+}  // namespace
+
+extern "C" int tw_transpose_bf16(const void* src, int64_t ld_src, int rows, int cols, void* dst, int64_t ld_dst,
+                                 hipStream_t stream) {
+  if (rows <= 0 || cols <= 0) return TW_OK;
+  const int vec = !(ld_src & 7) && !((uintptr_t)src & 15);     // 16-B row reads when aligned
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, stream,
+                     (const bf16*)src, ld_src, rows, cols, (bf16*)dst, ld_dst, vec);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+
 extern "C" int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
   if (n <= 0) return TW_OK;
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(nblocks(n / 4 + 1, 256)), dim3(256), 0, stream, src, (bf16*)dst, n);

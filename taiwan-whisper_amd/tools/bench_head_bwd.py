@@ -41,3 +41,22 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def vendor_nn():
+    """the same dX products (B MN-major) on hipBLASLt through torch.matmul, and the student decoder's dX shapes"""
+    for name, M, N, K in (("head dX", 28608, 1280, 51904), ("qkv dX", 28608, 1280, 3840),
+                          ("fc2 dX", 28608, 5120, 1280), ("out dX", 28608, 1280, 1280)):
+        g = torch.randn(M, K, device="cuda").bfloat16()
+        W = torch.randn(K, N, device="cuda").bfloat16()
+        out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        ours = timeit(lambda: ops.gemm(g, W, out, M, N, K, lda=K, ldb=N, ldc=N, b_trans=True, flags=ops.GEMM_ROUND))
+        lt = timeit(lambda: torch.matmul(g, W, out=out))
+        fl = 2.0 * M * N * K
+        print(f"NN {name:8s} ours {ours*1e3:8.1f} us {fl/ours/1e9:7.1f} TF/s   hipBLASLt {lt*1e3:8.1f} us "
+              f"{fl/lt/1e9:7.1f} TF/s", flush=True)
+        del g, W, out
+
+
+if __name__ == "__main__" and os.environ.get("VENDOR_NN"):
+    vendor_nn()

@@ -36,6 +36,7 @@ SIGNATURES = {
     "tw_embed_fwd": [P, P, I32, P, I32, P, I32, I32, I32, I32, I32, P],
     "tw_embed_bwd": [P, P, P, I32, I32, I64, P],
     "tw_cast_f32_bf16": [P, P, I64, P],
+    "tw_transpose_bf16": [P, I64, I32, I32, P, I64, P],
     "tw_colsum": [P, I32, I64, I32, I32, P, I32, I32, P, I64, P],
     "tw_l2norm": [P, I64, P, P, P],
     "tw_adamw": [P, P, P, P, P, I64, F32, F32, F32, F32, F32, I32, P, F32, P],

@@ -804,9 +804,15 @@ class Backward:
         M = h16.shape[0]
         E16 = m._w16("model.decoder.embed_tokens.weight")
         gE = m.gv("model.decoder.embed_tokens.weight")
-        # LM head (tied): dh = bf16(dlogits E), dE += bf16(dlogits^T h)
+        # LM head (tied): dh = bf16(dlogits E), dE += bf16(dlogits^T h).  On the bf16 path E goes K-major first
+        # (one 133 MB transpose): the K = 51 904 product then runs on the persistent kernel
         dh = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
-        F.gemm(dlogits, E16, dh, M, d, m.Vp, lda=m.Vp, ldb=d, ldc=d, b_trans=True, flags=F.GEMM_ROUND)
+        if E16.dtype == torch.bfloat16 and M >= 4096:
+            ET = F.transpose_bf16(E16, torch.empty(d, m.Vp, dtype=torch.bfloat16, device=self.dev))
+            F.gemm(dlogits, ET, dh, M, d, m.Vp, lda=m.Vp, ldb=m.Vp, ldc=d, flags=F.GEMM_ROUND)
+            del ET
+        else:
+            F.gemm(dlogits, E16, dh, M, d, m.Vp, lda=m.Vp, ldb=d, ldc=d, b_trans=True, flags=F.GEMM_ROUND)
         if gE is not None:
             F.gemm(dlogits, h16, gE, m.Vp, d, M, lda=m.Vp, ldb=d, ldc=d, a_trans=True, b_trans=True,
                    flags=F.GEMM_ROUND | F.GEMM_ACCUM)

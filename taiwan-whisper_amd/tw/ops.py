@@ -260,6 +260,16 @@ def embed_bwd(ids, dh, dE, padding_idx=-1):
     call("tw_embed_bwd", ids.data_ptr(), dh.data_ptr(), dE.data_ptr(), rows, D, int(padding_idx), _stream())
 
 
+def transpose_bf16(src, dst):
+    """dst [cols][rows] = src [rows][cols]^T (bf16, both row-major, dst contiguous)."""
+    rows, cols = src.shape
+    assert src.dtype == torch.bfloat16 and dst.dtype == torch.bfloat16 and src.stride(1) == 1
+    assert dst.is_contiguous() and tuple(dst.shape) == (cols, rows) and src.is_cuda and dst.is_cuda
+    _need(src, (rows - 1) * src.stride(0) + cols, "transpose src")
+    call("tw_transpose_bf16", src.data_ptr(), src.stride(0), rows, cols, dst.data_ptr(), rows, _stream())
+    return dst
+
+
 def cast_bf16(src, dst):
     assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() <= dst.numel()
     assert src.is_contiguous() and dst.is_contiguous()

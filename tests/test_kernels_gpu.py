@@ -380,6 +380,49 @@ def test_gemm_vendor_plain_forward(M, N, K, has_bias):
     assert (got[rows.to(DEV)].cpu() - want).abs().max() <= 2 ** -7 * want.abs().max()
 
 
+def test_gemm_vendor_mn_major_b():
+    """dX = dY . W products (MN-major B, K <= 8192) also run on hipBLASLt: within one bf16 ulp (+ the
+    cancellation term) of the 128x128 kernel and bit-identical on reruns."""
+    from tw import ops
+    M, N, K = 8192, 1280, 3840
+    g = torch.Generator(device=DEV).manual_seed(11)
+    dy = bf(torch.randn(M, K, device=DEV, generator=g))
+    W = bf(torch.randn(K, N, device=DEV, generator=g) * 0.05)
+    outs = []
+    for f in (ops.GEMM_TILE128, 0, 0):
+        C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(dy, W, C, M, N, K, lda=K, ldb=N, ldc=N, b_trans=True, flags=ops.GEMM_ROUND | f)
+        outs.append(C)
+    torch.cuda.synchronize()
+    ref, got = outs[0].float(), outs[1].float()
+    assert torch.equal(outs[1], outs[2]) and not torch.isnan(got).any()
+    tol = torch.maximum(got.abs(), ref.abs()) * 2 ** -7 + 2e-6 * float(ref.abs().max())
+    assert bool(((got - ref).abs() <= tol).all())
+
+
+def test_transpose_and_long_k_head_grad():
+    """The LM-head input gradient at the vocabulary K: E transposed to K-major (tw_transpose_bf16, exact,
+    ragged edges) and the K = 51 904 product on the persistent kernel == the MN-major product on the 128x128
+    kernel bit for bit (same K order)."""
+    from tw import ops
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for rows, cols in ((100, 70), (51904, 1280), (333, 1000)):
+        x = bf(torch.randn(rows, cols, device=DEV, generator=g))
+        y = ops.transpose_bf16(x, torch.empty(cols, rows, dtype=torch.bfloat16, device=DEV))
+        torch.cuda.synchronize()
+        assert torch.equal(y, x.t().contiguous()), (rows, cols)
+    M, d, V = 14000, 1280, 51904
+    dl = bf(torch.randn(M, V, device=DEV, generator=g))
+    E = bf(torch.randn(V, d, device=DEV, generator=g) * 0.05)
+    ET = ops.transpose_bf16(E, torch.empty(d, V, dtype=torch.bfloat16, device=DEV))
+    a = torch.empty(M, d, dtype=torch.bfloat16, device=DEV)
+    b = torch.empty(M, d, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(dl, ET, a, M, d, V, lda=V, ldb=V, ldc=d, flags=ops.GEMM_ROUND)                       # persistent
+    ops.gemm(dl, E, b, M, d, V, lda=V, ldb=d, ldc=d, b_trans=True, flags=ops.GEMM_ROUND | ops.GEMM_TILE128)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("N,K,M", [(1280, 1280, 28608), (2560, 1280, 8192), (264, 136, 4096), (1280, 1280, 1000)])
 def test_gemm_splitk_weight_grad(N, K, M):
     """dW[N][K] += round(dY^T X) with dY [M][N], X [M][K] (both MN-major operands, fp32 accumulate): the
