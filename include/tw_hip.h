@@ -72,12 +72,13 @@ int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_
  * Replaces nn.LayerNorm at HF modeling_whisper.py:392,402,470,485,498,642,790 (autocast fp32 op). */
 int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, const float* b, void* y, int y_dtype,
                      float* mean_out, float* rstd_out, int rows, int D, float eps, tw_stream_t stream);
-/* Residual add fused into the LayerNorm that follows it (fp32 residual stream, D % 256 == 0):
- * x_out = x + r (r = the preceding Linear's bf16 output: the HF residual `hidden_states = residual +
- * hidden_states` at modeling_whisper.py:399,412 / 479,495,506 under autocast), y = bf16 LayerNorm(x_out).
- * x_out may alias x.  Bit-identical to tw_gemm_bf16's residual epilogue followed by tw_layernorm_fwd. */
-int tw_add_layernorm_fwd(const float* x, const void* r, float* x_out, const float* w, const float* b, void* y,
-                         float* mean_out, float* rstd_out, int rows, int D, float eps, tw_stream_t stream);
+/* Residual add fused into the LayerNorm that follows it (D % 256 == 0, 16-B aligned rows): x_out = x + r
+ * (r = the preceding Linear's bf16 output: the HF residual `hidden_states = residual + hidden_states` at
+ * modeling_whisper.py:399,412 / 479,495,506; fp32 stream x_dtype 0 under autocast, bf16 stream x_dtype 1
+ * rounded once), y = bf16 LayerNorm(x_out).  x_out may alias x.  Bit-identical to tw_gemm_bf16's residual
+ * epilogue followed by tw_layernorm_fwd. */
+int tw_add_layernorm_fwd(const void* x, int x_dtype, const void* r, void* x_out, const float* w, const float* b,
+                         void* y, float* mean_out, float* rstd_out, int rows, int D, float eps, tw_stream_t stream);
 int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd, const void* dy,
                      int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out, int rows, int D,
                      float* workspace, int64_t workspace_floats, tw_stream_t stream);

@@ -84,11 +84,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 // bf16 -> bf16 rows with D % 256 == 0 (the teacher's bf16 residual stream): a half-wave per row
 // (8 rows per 256-thread block), NCH chunks of 8 bf16 per lane as 16-B loads / stores, statistics
 // reduced over the 32 lanes of the half (same two-pass mean / variance as ln_fwd_kernel).
-template <int NCH>
+// ADD: x_out = bf16(x + r) first (the bf16 stream's residual update, the same fp32 add + one round as the
+// GEMM's residual epilogue), then the LayerNorm of x_out.
+template <int NCH, bool ADD = false>
 __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ b, bf16* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                          int rows, int D, float eps) {
+                                                          int rows, int D, float eps, const bf16* __restrict__ r = nullptr,
+                                                          bf16* x_out = nullptr) {
   const int lane = lane_id(), hl = lane & 31;
   const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   const bool ok = row < rows;
@@ -98,7 +101,13 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int e = (c * 32 + hl) * 8;
-    const bf16x8 t = ok ? *(const bf16x8*)(x + base + e) : bf16x8{};
+    bf16x8 t = ok ? *(const bf16x8*)(x + base + e) : bf16x8{};
+    if constexpr (ADD) {
+      const bf16x8 u = ok ? *(const bf16x8*)(r + base + e) : bf16x8{};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = f2bf(bf2f(t[q]) + bf2f(u[q]));
+      if (ok) *(bf16x8*)(x_out + base + e) = t;
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) { v[c][q] = bf2f(t[q]); s += v[c][q]; }
   }
@@ -265,15 +274,34 @@ extern "C" int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, cons
   return TW_OK;
 }
 
-extern "C" int tw_add_layernorm_fwd(const float* x, const void* r, float* x_out, const float* w, const float* b,
-                                    void* y, float* mean_out, float* rstd_out, int rows, int D, float eps,
-                                    hipStream_t stream) {
+extern "C" int tw_add_layernorm_fwd(const void* x, int x_dtype, const void* r, void* x_out, const float* w,
+                                    const float* b, void* y, float* mean_out, float* rstd_out, int rows, int D,
+                                    float eps, hipStream_t stream) {
   if (rows <= 0) return TW_OK;
   if (D % 256 || D > 1280) return TW_EUNSUPPORTED;
-  if ((((uintptr_t)x | (uintptr_t)r | (uintptr_t)x_out | (uintptr_t)y) & 15) != 0) return TW_EINVAL;
-  hipLaunchKernelGGL((ln_fwd_kernel<4, 5, true>), dim3((rows + WPB - 1) / WPB), dim3(64 * WPB), 0, stream,
-                     (const void*)x, (int)TW_F32, w, b, y, (int)TW_BF16, mean_out, rstd_out, rows, D, eps,
-                     (const bf16*)r, x_out);
+  if ((((uintptr_t)x | (uintptr_t)r | (uintptr_t)x_out | (uintptr_t)y | (uintptr_t)w | (uintptr_t)b) & 15) != 0)
+    return TW_EINVAL;
+  if (x_dtype == TW_F32) {
+    hipLaunchKernelGGL((ln_fwd_kernel<4, 5, true>), dim3((rows + WPB - 1) / WPB), dim3(64 * WPB), 0, stream, x,
+                       (int)TW_F32, w, b, y, (int)TW_BF16, mean_out, rstd_out, rows, D, eps, (const bf16*)r,
+                       (float*)x_out);
+  } else {
+    const dim3 g2((rows + 2 * WPB - 1) / (2 * WPB)), block(64 * WPB);
+    const bf16 *xb = (const bf16*)x, *rb = (const bf16*)r;
+    bf16 *yb = (bf16*)y, *xo = (bf16*)x_out;
+    switch (D / 256) {
+      case 1: hipLaunchKernelGGL((ln_fwd_bf16_kernel<1, true>), g2, block, 0, stream, xb, w, b, yb, mean_out, rstd_out,
+                                 rows, D, eps, rb, xo); break;
+      case 2: hipLaunchKernelGGL((ln_fwd_bf16_kernel<2, true>), g2, block, 0, stream, xb, w, b, yb, mean_out, rstd_out,
+                                 rows, D, eps, rb, xo); break;
+      case 3: hipLaunchKernelGGL((ln_fwd_bf16_kernel<3, true>), g2, block, 0, stream, xb, w, b, yb, mean_out, rstd_out,
+                                 rows, D, eps, rb, xo); break;
+      case 4: hipLaunchKernelGGL((ln_fwd_bf16_kernel<4, true>), g2, block, 0, stream, xb, w, b, yb, mean_out, rstd_out,
+                                 rows, D, eps, rb, xo); break;
+      default: hipLaunchKernelGGL((ln_fwd_bf16_kernel<5, true>), g2, block, 0, stream, xb, w, b, yb, mean_out, rstd_out,
+                                  rows, D, eps, rb, xo); break;
+    }
+  }
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

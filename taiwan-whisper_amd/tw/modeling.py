@@ -436,14 +436,15 @@ class WhisperForConditionalGeneration:
         F.layernorm_fwd(x, self.ln_param(name + ".weight"), self.ln_param(name + ".bias"), y, mean, rstd)
         return y
 
-    @property
-    def defer_residual(self):
-        """fp32 residual stream under autocast (the student): the stream-updating Linears (out_proj, fc2)
-        write their bf16 output and the next LayerNorm adds it to the stream (tw_add_layernorm_fwd, the same
-        fp32 add): the fp32 read-modify-write leaves the persistent GEMM's epilogue.
-        TW_DEFER_RES=0 keeps it in the epilogue (A/B runs)."""
-        return (self.stream_dtype == torch.float32 and self.act_dtype == torch.bfloat16
-                and self.config.d_model % 256 == 0 and _DEFER_RES)
+    def defer_residual(self, kind):
+        """Whether the stream-updating Linear of a `kind` block ("attn" = out_proj, "mlp" = fc2) writes its bf16
+        output and leaves the residual add to the next LayerNorm (tw_add_layernorm_fwd, the same add): on the
+        student's fp32 stream for both (the fp32 read-modify-write leaves the persistent GEMM's epilogue), on
+        the bf16 teacher stream for out_proj only (the plain projection then runs on hipBLASLt; at fc2 the extra
+        LN traffic costs what the epilogue saves).  DESIGN.md §5; TW_DEFER_RES=0 disables (A/B runs)."""
+        if not _DEFER_RES or self.act_dtype != torch.bfloat16 or self.config.d_model % 256:
+            return False
+        return self.stream_dtype == torch.float32 or kind == "attn"
 
     def _ln_in(self, x, pend, name, save):
         """Block-entry LayerNorm -> (stream, LN output).  pend: a deferred residual update (bf16), added to
@@ -460,11 +461,11 @@ class WhisperForConditionalGeneration:
         F.add_layernorm_fwd(x, pend, xn, self.ln_param(name + ".weight"), self.ln_param(name + ".bias"), y, mean, rstd)
         return xn, y
 
-    def _res_out(self, h, w, b, x, tape):
-        """The stream-updating Linear -> (stream, pending update): deferred to the next LayerNorm on fp32
-        streams, else applied by the GEMM's residual epilogue."""
+    def _res_out(self, h, w, b, x, tape, kind):
+        """The stream-updating Linear -> (stream, pending update): deferred to the next LayerNorm
+        (defer_residual), else applied by the GEMM's residual epilogue."""
         M, N = h.shape[0], w.shape[0]
-        if self.defer_residual:
+        if self.defer_residual(kind):
             r = torch.empty(M, N, dtype=self.act_dtype, device=self.device)
             self._lin(h, w, b, r)
             return x, r
@@ -486,7 +487,7 @@ class WhisperForConditionalGeneration:
         o = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         lse = torch.empty(B * H * T, dtype=torch.float32, device=self.device) if tape is not None else None
         F.attn_fwd(qkv, 3 * d, qkv[:, d:], 3 * d, qkv[:, 2 * d:], 3 * d, o, d, lse, B, H, T, T, causal, 0.125)
-        out = self._res_out(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), x, tape)
+        out = self._res_out(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), x, tape, "attn")
         if tape is not None:
             tape.append(("attn", p, dict(sv=sv, y=y, qkv=qkv, o=o, lse=lse, B=B, T=T, causal=causal)))
         return out
@@ -507,7 +508,7 @@ class WhisperForConditionalGeneration:
         o = torch.empty(M, d, dtype=self.act_dtype, device=self.device)
         lse = torch.empty(B * H * T, dtype=torch.float32, device=self.device) if tape is not None else None
         F.attn_fwd(q, d, kv, 2 * d, kv[:, d:], 2 * d, o, d, lse, B, H, T, Tk, False, 0.125)
-        out = self._res_out(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), x, tape)
+        out = self._res_out(o, self._w16(p + ".out_proj.weight"), self._w16(p + ".out_proj.bias"), x, tape, "attn")
         if tape is not None:
             tape.append(("cross", p, dict(sv=sv, y=y, q=q, kv=kv, o=o, lse=lse, B=B, T=T, Tk=Tk)))
         return out
@@ -521,7 +522,7 @@ class WhisperForConditionalGeneration:
         pre = torch.empty(M, f, dtype=self.act_dtype, device=self.device) if tape is not None else None
         self._lin(y, self._w16(p + ".fc1.weight"), self._w16(p + ".fc1.bias"), h, aux=pre,
                   flags=F.GEMM_ROUND | F.GEMM_GELU | (F.GEMM_AUX_OUT if tape is not None else 0))
-        out = self._res_out(h, self._w16(p + ".fc2.weight"), self._w16(p + ".fc2.bias"), x, tape)
+        out = self._res_out(h, self._w16(p + ".fc2.weight"), self._w16(p + ".fc2.bias"), x, tape, "mlp")
         if tape is not None:
             tape.append(("mlp", p, dict(sv=sv, y=y, h=h, pre=pre)))
         return out

@@ -535,14 +535,15 @@ def test_layernorm(D, xdt):
 
 
 @pytest.mark.parametrize("D", [768, 1280])
-def test_add_layernorm_matches_residual_epilogue(D):
-    """Deferred residual update (fp32 stream): the Linear's bf16 output r added by the next LayerNorm
-    (tw_add_layernorm_fwd) == the GEMM's residual epilogue followed by tw_layernorm_fwd, bit for bit,
-    in place and into a separate stream buffer."""
+@pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])
+def test_add_layernorm_matches_residual_epilogue(D, sdt):
+    """Deferred residual update (fp32 student stream, bf16 teacher stream): the Linear's bf16 output r added
+    by the next LayerNorm (tw_add_layernorm_fwd) == the GEMM's residual epilogue followed by tw_layernorm_fwd,
+    bit for bit, in place and into a separate stream buffer."""
     from tw import ops
     g = torch.Generator().manual_seed(D + 1)
     rows, K = 1000, 256
-    x0 = (torch.randn(rows, D, generator=g) * 3).to(DEV)
+    x0 = (torch.randn(rows, D, generator=g) * 3).to(DEV).to(sdt)
     A, W = bf(torch.randn(rows, K, generator=g)).to(DEV), bf(torch.randn(D, K, generator=g) * 0.1).to(DEV)
     bias = bf(torch.randn(D, generator=g)).to(DEV)
     w, b = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
