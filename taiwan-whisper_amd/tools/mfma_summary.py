@@ -26,7 +26,7 @@ FAMILIES = [
     ("gemm_pp (persistent 256x256 forward GEMM)", r"gemm_pp_kernel"),
     ("gemm 128x128 / 256 tiles (small-grid fwd, dX, dW)", r"gemm_kernel<"),
     ("gemm skinny (decode)", r"gemm_skinny"),
-    ("hipBLASLt (plain projections)", r"^Cijk_"),
+    ("hipBLASLt (plain projections)", r"Cijk_"),
     ("attention fwd", r"attn_fwd"),
     ("attention bwd", r"attn_bwd"),
     ("fp32 gemm", r"gemm_f32|f32_gemm"),

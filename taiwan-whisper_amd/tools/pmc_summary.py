@@ -23,7 +23,7 @@ FAMILIES = {
     "gemm_nn": r"gemm_kernel<false, false|gemm_pp_kernel",
     "gemm_nt": r"gemm_kernel<false, true",
     "gemm_tt": r"gemm_kernel<true, true",
-    "vendor_gemm": r"^Cijk_",                     # hipBLASLt kernels (csrc/gemm_vendor.hip)
+    "vendor_gemm": r"Cijk_",                     # hipBLASLt kernels (csrc/gemm_vendor.hip)
     "attn_fwd": r"attn_fwd_kernel",
     "klce": r"klce_kernel",
     "ln_fwd": r"ln_fwd_kernel",
