@@ -428,11 +428,12 @@ __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
   const int wrow = n0 + li;
   const bool wok = wrow < p.N;
   const bf16* wp = p.B + (int64_t)(wok ? wrow : 0) * p.ldb + 8 * g;
+  const int mbase = (int)blockIdx.z * MF * 16;              // row block (batches of 65..128 rows: 2 x 64)
   const bf16* ap[MF];
   bool aok[MF];
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
-    const int m = i * 16 + li;
+    const int m = mbase + i * 16 + li;
     aok[i] = m < p.M;
     ap[i] = p.A + (int64_t)(aok[i] ? m : 0) * p.lda + 8 * g;
   }
@@ -478,9 +479,9 @@ __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
     for (int r = 0; r < 4; ++r) part[wave][i * 16 + li][4 * g + r] = acc[i][r];
   __syncthreads();
   for (int e = threadIdx.x; e < MF * 16 * 16; e += 256) {
-    const int m = e >> 4, c = e & 15, n = n0 + c;
+    const int ml = e >> 4, c = e & 15, n = n0 + c, m = mbase + ml;
     if (m < p.M && n < p.N) {
-      const float v = part[0][m][c] + part[1][m][c] + part[2][m][c] + part[3][m][c];
+      const float v = part[0][ml][c] + part[1][ml][c] + part[2][ml][c] + part[3][ml][c];
       if (p.ws) p.ws[((int64_t)blockIdx.y * p.M + m) * p.N + n] = v;
       else epi_element(p, m, n, v);
     }
@@ -666,9 +667,19 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
   }
 }
 
+// Row blocks per skinny launch: batches of 65..128 rows run as 2 blocks of 64 (blockIdx.z) -- the
+// 128-row form loads 8 A fragments per W fragment and measured 18 / 31 us on the large-v2 decode
+// out_proj / fc2 at M = 128 against 14.5 / 18 us at M = 64 (tools/bench_decode_gemm.py); W is then read
+// twice, the second time from L2.  TW_SKINNY_ZSPLIT=0 keeps the single 128-row block (A/B runs).
+int skinny_row_blocks(int M) {
+  static const int env = [] { const char* e = getenv("TW_SKINNY_ZSPLIT"); return e ? atoi(e) : 1; }();
+  return (env && M > 64) ? 2 : 1;
+}
+
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
-  const dim3 grid((p.N + 15) / 16, S);
-  const int mf = (p.M + 15) / 16;
+  const int zb = skinny_row_blocks(p.M);
+  const dim3 grid((p.N + 15) / 16, S, zb);
+  const int mf = zb > 1 ? 4 : (p.M + 15) / 16;
   switch (mf) {
     case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, stream, p); break;
     case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, stream, p); break;
@@ -969,7 +980,7 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
     // also split over workgroups (chunks of >= 4 k-steps) into fp32 partials, reduced with the
     // epilogue (c4 batch 64 / 128: -3 / -4 % per step; at batch 1 the extra launch loses 9 %).
     p.ws = nullptr;
-    const int nwg = (N + 15) / 16, nk = (K + 31) / 32;
+    const int nwg = (N + 15) / 16 * skinny_row_blocks(M), nk = (K + 31) / 32;
     int S = std::min((512 + nwg - 1) / nwg, nk / 4);
     if ((flags & 16384) || M <= 32) S = 1;          // small batches: the reduce launch costs more than it saves
     void* ws = S > 1 ? splitk_workspace(stream, (size_t)S * M * N * sizeof(float)) : nullptr;
