@@ -671,15 +671,25 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
 // 128-row form loads 8 A fragments per W fragment and measured 18 / 31 us on the large-v2 decode
 // out_proj / fc2 at M = 128 against 14.5 / 18 us at M = 64 (tools/bench_decode_gemm.py); W is then read
 // twice, the second time from L2.  TW_SKINNY_ZSPLIT=0 keeps the single 128-row block (A/B runs).
+// TW_SKINNY_ROWS (16 / 32 / 64, A/B runs): rows per block for batches above it.
+int skinny_block_rows() {
+  static const int r = [] {
+    const char* e = getenv("TW_SKINNY_ROWS");
+    const int v = e ? atoi(e) : 64;
+    return (v == 16 || v == 32 || v == 64) ? v : 64;
+  }();
+  return r;
+}
 int skinny_row_blocks(int M) {
   static const int env = [] { const char* e = getenv("TW_SKINNY_ZSPLIT"); return e ? atoi(e) : 1; }();
-  return (env && M > 64) ? 2 : 1;
+  const int R = skinny_block_rows();
+  return (env && M > R) ? (M + R - 1) / R : 1;
 }
 
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
   const int zb = skinny_row_blocks(p.M);
   const dim3 grid((p.N + 15) / 16, S, zb);
-  const int mf = zb > 1 ? 4 : (p.M + 15) / 16;
+  const int mf = zb > 1 ? skinny_block_rows() / 16 : (p.M + 15) / 16;
   switch (mf) {
     case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, stream, p); break;
     case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, stream, p); break;
