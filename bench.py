@@ -289,7 +289,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-teacher-fwd", action="store_true")
     args = ap.parse_args()
-    dflt = {"c3": (64, 10, 3), "c2": (32, 10, 3), "c4": (128, 4, 1), "c5": (1, 1, 1)}[args.config]
+    dflt = {"c3": (64, 10, 3), "c2": (32, 10, 3), "c4": (512, 1, 1), "c5": (1, 1, 1)}[args.config]
     args.batch = dflt[0] if args.batch is None else args.batch
     args.steps = dflt[1] if args.steps is None else args.steps
     args.warmup = dflt[2] if args.warmup is None else args.warmup

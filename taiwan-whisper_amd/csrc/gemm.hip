@@ -983,7 +983,11 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
   // decode-step GEMMs (tools/bench_skinny.py, r01): the weight-streaming kernel wins for N <= 3840
   // (and N <= 8192 at M <= 64); the LM head and wide M=128 GEMMs stream faster as 128x128 tiles
-  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && (N <= 4096 || (M <= 64 && N <= 8192)) &&
+  // TW_SKINNY_MAXM (A/B runs): row-blocked skinny launches above 128 rows too.  Measured at M = 512
+  // (tools/bench_decode_gemm.py): qkv 50 vs 21 us, fc2 69 vs 60 us against the 128x128 tiles, so 128 stays.
+  static const int skinny_max_m = [] { const char* e = getenv("TW_SKINNY_MAXM"); return e ? atoi(e) : 128; }();
+  const int max_m = skinny_row_blocks(M) > 1 ? std::max(128, skinny_max_m) : 128;
+  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= max_m && (N <= 4096 || (M <= 64 && N <= 8192)) &&
                       !(flags & (256 | 512 | 1024 | 2048));
   if (skinny && ((uintptr_t)A & 15) == 0) {
     // decode-step GEMMs: stream W once.  With fewer than 512 workgroups and M > 32 the K range is

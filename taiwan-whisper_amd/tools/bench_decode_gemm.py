@@ -15,7 +15,7 @@ SHAPES = [("qkv", 3840, 1280), ("out/xq", 1280, 1280), ("fc1", 5120, 1280), ("fc
 
 
 def main():
-    for M in (128, 64, 32):
+    for M in (512, 256, 128):
         for name, N, K in SHAPES:
             A = torch.randn(M, K, device="cuda").bfloat16()
             W = torch.randn(N, K, device="cuda").bfloat16()

@@ -454,10 +454,11 @@ def test_gemm_splitk_weight_grad(N, K, M):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 16, 8), (5, 1000, 1280), (64, 1281 - 1, 5120), (100, 3840, 1280),
-                                   (128, 200, 64), (128, 1280, 5120), (65, 520, 1280)])
+                                   (128, 200, 64), (128, 1280, 5120), (65, 520, 1280), (512, 1280, 1280),
+                                   (300, 3840, 1280)])
 def test_gemm_skinny_decode_path(M, N, K):
-    """M <= 128 K-major GEMMs (decode steps) take the weight-streaming kernel (65..128 rows as two 64-row
-    blocks, the second ragged for M < 128); every epilogue kind against fp64 (tolerance: one bf16 ulp of
+    """M <= 512 K-major GEMMs (decode steps) take the weight-streaming kernel (above 64 rows as 64-row
+    blocks, the last one ragged unless M % 64 == 0); every epilogue kind against fp64 (tolerance: one bf16 ulp of
     the largest value; fp32 out 1e-5 relative)."""
     from tw import ops
     g = torch.Generator().manual_seed(M * 7 + N + K)
