@@ -860,6 +860,15 @@ int sk_tail_plan(const GemmP& p, int batch, int& m_dp) {
   const int G = pp_grid_cus();
   const int tn = (p.N + 255) / 256, tm = (p.M + 255) / 256;
   const int64_t T = (int64_t)tn * tm;
+  if (T < G && p.M >= 256) {
+    // less than one round (the decode step's fc2 at a 512-clip batch: 10 tiles of K = 5120, 60 us on 40
+    // 128x128 tiles): every tile split into up to 16 K-chunks, no whole-round part
+    m_dp = 0;
+    int best = 0;
+    for (int S = 2; S <= 16; ++S)
+      if (p.K % (64 * S) == 0 && T * S <= G && p.K / S >= 256) best = S;
+    return best;
+  }
   if (T < G || T >= 4 * G) return 0;                  // < 1 round: nothing to fill; many rounds: tail small
   m_dp = (int)((T / G) * G / tn);                      // m-tile rows of whole rounds
   const int tail = (tm - m_dp) * tn;
@@ -875,10 +884,12 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
   const size_t bytes = (size_t)S * Mt * p.N * sizeof(float);
   float* ws = (float*)splitk_workspace(stream, bytes);
   if (!ws) return 0;
-  GemmP d = p;                                         // whole rounds: the unsplit kernel
-  d.M = m_dp * 256;
-  launch_pp(d, 1, stream);
-  TW_CHECK_LAUNCH();
+  if (m_dp > 0) {
+    GemmP d = p;                                       // whole rounds: the unsplit kernel
+    d.M = m_dp * 256;
+    launch_pp(d, 1, stream);
+    TW_CHECK_LAUNCH();
+  }
   GemmP q = p;                                         // tail rows: S K-chunks -> fp32 partials
   const int64_t r0 = (int64_t)m_dp * 256;
   q.A = p.A + r0 * p.lda;

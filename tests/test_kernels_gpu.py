@@ -291,11 +291,12 @@ def test_gemm_pp_grouped_tile_order():
     assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
 
 
-@pytest.mark.parametrize("M,N,K", [(28608, 1280, 5120), (11000, 1288, 4096)])
+@pytest.mark.parametrize("M,N,K", [(28608, 1280, 5120), (11000, 1288, 4096), (512, 1280, 5120)])
 def test_gemm_sk_tail_forward(M, N, K):
     """Mid-sized long-K forward GEMMs (1-4 rounds of 256-tiles, K >= 3072: the decoder's fc2 at B = 64) take
     whole rounds on the persistent kernel and the remaining m-tile rows as split-K chunks + an ordered
-    fp32 reduce with the full epilogue.  Rows of the whole rounds equal the 128x128 kernel bit for bit
+    fp32 reduce with the full epilogue; below one round (M >= 256: the decode step's fc2 at a 512-clip
+    batch) every row is a split-K row.  Rows of the whole rounds equal the 128x128 kernel bit for bit
     (same K order); the tail rows regroup the fp32 sum by chunk, so they may sit one bf16 ulp away (the
     rounding boundary) — checked against the 128x128 kernel and fp64 on sampled rows.  Epilogues: bias +
     round, bias + round + GELU with the pre-activation aux, in-place bf16 residual."""
@@ -323,8 +324,8 @@ def test_gemm_sk_tail_forward(M, N, K):
     torch.cuda.synchronize()
     cus = torch.cuda.get_device_properties(0).multi_processor_count & ~7
     tn, tm = (N + 255) // 256, (M + 255) // 256
-    m_dp = (tn * tm // cus) * cus // tn * 256                # rows of the whole rounds
-    assert 0 < m_dp < M
+    m_dp = (tn * tm // cus) * cus // tn * 256                # rows of the whole rounds (0 below one round)
+    assert 0 <= m_dp < M
     same_pre = outs["sk"]["aux"][m_dp:] == outs["t128"]["aux"][m_dp:]
     for kind in ("bf16", "gelu", "aux", "res_bf16"):
         got, ref = outs["sk"][kind], outs["t128"][kind]
