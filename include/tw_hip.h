@@ -205,6 +205,12 @@ int tw_token_logprob(const void* logits, int64_t ld, int logits_dtype, int B, in
                      tw_stream_t stream);
 int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype, const void* pos, int pos_dtype, void* out,
                   int out_dtype, int B, int D, const int* t_dev, tw_stream_t stream);
+/* tw_kv_head_major: the cross-attention K/V as the KV projection writes it (rows b*Tk + t of [B*Tk][ld], k at
+ * columns 0..64H, v at 64H..128H) -> dst = K [B][H][Tk][64] followed by V [B][H][Tk][64], so tw_decode_attn reads
+ * each (clip, head) as two contiguous runs (called as B*H one-head clips: ldk = 64, skb = Tk*64).  Replaces the
+ * layout of HF's cross-attention past_key_values ([B][H][Tk][64], modeling_whisper.py WhisperAttention).  dtype bf16
+ * or f32; ld a multiple of 16 B. */
+int tw_kv_head_major(const void* src, int64_t ld, void* dst, int B, int Tk, int H, int dtype, tw_stream_t stream);
 int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n, int dtype,
                  const int* t_dev, tw_stream_t stream);
 int tw_step_advance(int* t_dev, int by, tw_stream_t stream);

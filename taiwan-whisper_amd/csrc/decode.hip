@@ -22,6 +22,7 @@
 //  * tw_token_logprob: log-softmax of a raw logits row at one id (WhisperNoSpeechDetection).
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -774,6 +775,45 @@ extern "C" int tw_embed_step(const int64_t* ids, const void* tok, int tok_dtype,
   if (!t_dev || D <= 0) return TW_EINVAL;
   hipLaunchKernelGGL(embed_step_kernel, dim3(B), dim3(256), 0, stream, ids, tok, tok_dtype, pos, pos_dtype, out,
                      out_dtype, D, t_dev);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+// cross-attention K/V, row-interleaved [rows = B*Tk][ld] (k at columns 0..d, v at d..2d, head h at 64h..) ->
+// head-major dst: K [B][H][Tk][64] then V [B][H][Tk][64] (one (clip, head) reads two contiguous Tk*64 runs)
+template <typename E>
+__global__ void kv_head_major_kernel(const E* __restrict__ src, int64_t ld, E* __restrict__ dst, int Tk, int H,
+                                     int64_t rows) {
+  constexpr int W = 16 / sizeof(E);
+  const int d = H * 64, nv = 2 * d / W;                     // 16-B vectors per source row
+  const int64_t total = rows * nv;
+  const int64_t half = rows * d;                            // elements of the K part
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nv;
+    const int c = (int)(i - r * nv) * W;                    // source column
+    const int part = c >= d, cc = c - part * d, h = cc >> 6, e = cc & 63;
+    const int64_t b = r / Tk, t = r - b * Tk;
+    const int4 v = *(const int4*)(src + r * ld + c);
+    *(int4*)(dst + part * half + ((b * H + h) * Tk + t) * 64 + e) = v;
+  }
+}
+
+extern "C" int tw_kv_head_major(const void* src, int64_t ld, void* dst, int B, int Tk, int H, int dtype,
+                                hipStream_t stream) {
+  if (B <= 0 || Tk <= 0 || H <= 0) return TW_OK;
+  const int w = dtype == TW_F32 ? 3 : 7;
+  if ((ld & w) || ld < 2 * 64 * H || (((uintptr_t)src | (uintptr_t)dst) & 15)) return TW_EINVAL;
+  const int64_t rows = (int64_t)B * Tk;
+  const int64_t nvec = rows * (2 * 64 * H) / (w + 1);
+  const dim3 grid((unsigned)std::min<int64_t>((nvec + 255) / 256, 16384));
+  if (dtype == TW_BF16)
+    hipLaunchKernelGGL(kv_head_major_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)src, ld, (bf16*)dst, Tk, H,
+                       rows);
+  else if (dtype == TW_F32)
+    hipLaunchKernelGGL(kv_head_major_kernel<float>, grid, dim3(256), 0, stream, (const float*)src, ld, (float*)dst,
+                       Tk, H, rows);
+  else
+    return TW_EUNSUPPORTED;
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

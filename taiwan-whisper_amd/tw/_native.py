@@ -54,6 +54,7 @@ SIGNATURES = {
     "tw_token_logprob": [P, I64, I32, I32, I32, I32, P, P],
     "tw_embed_step": [P, P, I32, P, I32, P, I32, I32, I32, P, P],
     "tw_kv_append": [P, I64, P, I64, I64, I32, I32, I32, P, P],
+    "tw_kv_head_major": [P, I64, P, I32, I32, I32, I32, P],
     "tw_step_advance": [P, I32, P],
     # fp32 arithmetic path
     "tw_gemm_f32": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I64, I64, I64, I32, I64, I64, I64, F32,

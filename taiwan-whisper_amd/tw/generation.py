@@ -23,9 +23,13 @@ replayed per token; the host reads the finished flags every 8 steps to stop earl
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops as F
+
+_XKV_HEAD_MAJOR = os.environ.get("TW_XKV_HEAD_MAJOR", "0") != "0"
 
 
 class DecodeSession:
@@ -42,8 +46,18 @@ class DecodeSession:
         act = model.act_dtype            # bf16 (autocast) or fp32 (fp32 path): caches, operands, logits
         self.self_kv = [torch.empty(B, T_max, 2 * d, dtype=act, device=dev)
                         for _ in range(cfg.decoder_layers)]
-        self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
-                         for _ in range(cfg.decoder_layers)]
+        # cross-attention K/V head-major (K [B][H][Tk][64] then V): each (clip, head) of the per-step
+        # cross-attention reads two contiguous runs instead of 128-B rows 2d apart (tw_kv_head_major; the
+        # projection goes through one scratch [B*Tk][2d] block).  TW_XKV_HEAD_MAJOR=0: the projection's own
+        # row-interleaved layout.
+        self.hm = _XKV_HEAD_MAJOR
+        if self.hm:
+            self.cross_kv = [torch.empty(2 * B * self.H * Tk * 64, dtype=act, device=dev)
+                             for _ in range(cfg.decoder_layers)]
+            self._kv_proj = torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
+        else:
+            self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
+                             for _ in range(cfg.decoder_layers)]
         self.set_encoder(enc16)
         self.t_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cur = torch.zeros(B, dtype=torch.int64, device=dev)       # this step's input ids
@@ -68,7 +82,11 @@ class DecodeSession:
             p = f"model.decoder.layers.{i}.encoder_attn"
             wkv = m.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
             bkv = m.wspan(p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
-            m._lin(enc16, wkv, bkv, kv)
+            if self.hm:
+                m._lin(enc16, wkv, bkv, self._kv_proj)
+                F.kv_head_major(self._kv_proj, 2 * d, kv, self.B, self.Tk, self.H)
+            else:
+                m._lin(enc16, wkv, bkv, kv)
 
     def _ln(self, x, name):
         m = self.m
@@ -127,8 +145,13 @@ class DecodeSession:
             self._ln_lin(x, p + ".encoder_attn_layer_norm", m._w16(p + ".encoder_attn.q_proj.weight"),
                          m._w16(p + ".encoder_attn.q_proj.bias"), self.q)
             kv = self.cross_kv[i]
-            F.decode_attn(self.q, d, kv, 2 * d, self.Tk * 2 * d, kv[:, d:], 2 * d, self.Tk * 2 * d, o, d, B, H,
-                          self.Tk, 0.125)
+            if self.hm:         # B*H one-head clips over contiguous [Tk][64] runs
+                hv = B * H * self.Tk * 64
+                F.decode_attn(self.q, 64, kv, 64, self.Tk * 64, kv[hv:], 64, self.Tk * 64, o, 64, B * H, 1,
+                              self.Tk, 0.125)
+            else:
+                F.decode_attn(self.q, d, kv, 2 * d, self.Tk * 2 * d, kv[:, d:], 2 * d, self.Tk * 2 * d, o, d, B, H,
+                              self.Tk, 0.125)
             self._lin(o, m._w16(p + ".encoder_attn.out_proj.weight"), m._w16(p + ".encoder_attn.out_proj.bias"), x,
                       res=x)
             # MLP

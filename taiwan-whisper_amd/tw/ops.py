@@ -489,6 +489,14 @@ def kv_append(src, ld_src, cache, ld_row, sb, B, n, t_dev, max_rows):
          _stream())
 
 
+def kv_head_major(src, ld, dst, B, Tk, H):
+    """Row-interleaved cross K/V [B*Tk][ld] -> head-major K [B][H][Tk][64] then V (include/tw_hip.h)."""
+    assert src.dtype == dst.dtype and src.dtype in (torch.bfloat16, torch.float32)
+    _need(src, (B * Tk - 1) * ld + 2 * 64 * H, "kv_head_major src")
+    _need(dst, 2 * B * H * Tk * 64, "kv_head_major dst")
+    call("tw_kv_head_major", src.data_ptr(), ld, dst.data_ptr(), B, Tk, H, _dt(src), _stream())
+
+
 def step_advance(t_dev, by=1):
     assert t_dev.dtype == torch.int32 and t_dev.is_cuda
     call("tw_step_advance", t_dev.data_ptr(), int(by), _stream())

@@ -63,6 +63,29 @@ def test_decode_attn(B, H, Tk, dev):
     assert err.max() <= 2 ** -7 * ref.abs().max() + 1e-3
 
 
+@pytest.mark.parametrize("B,Tk,H,dt", [(3, 1500, 20, torch.bfloat16), (2, 7, 2, torch.float32), (1, 1500, 6, torch.bfloat16)])
+def test_kv_head_major(B, Tk, H, dt):
+    """tw_kv_head_major is the exact permutation [B*Tk][k | v] -> K [B][H][Tk][64], V [B][H][Tk][64] (a padded
+    source row stride included), and decode attention over it (B*H one-head clips) equals the row-interleaved
+    call bit for bit."""
+    from tw import ops
+    d = 64 * H
+    ld = 2 * d + 8
+    src = torch.randn(B * Tk, ld, device=DEV).to(dt)
+    dst = torch.full((2 * B * H * Tk * 64,), float("nan"), device=DEV).to(dt)
+    ops.kv_head_major(src, ld, dst, B, Tk, H)
+    want_k = src[:, :d].reshape(B, Tk, H, 64).transpose(1, 2).reshape(-1)
+    want_v = src[:, d:2 * d].reshape(B, Tk, H, 64).transpose(1, 2).reshape(-1)
+    half = B * H * Tk * 64
+    assert torch.equal(dst[:half], want_k) and torch.equal(dst[half:], want_v)
+    q = torch.randn(B, d, device=DEV).to(dt)
+    o_row = torch.empty(B, d, device=DEV).to(dt)
+    o_hm = torch.empty(B, d, device=DEV).to(dt)
+    ops.decode_attn(q, d, src, ld, Tk * ld, src[:, d:], ld, Tk * ld, o_row, d, B, H, Tk, 0.125)
+    ops.decode_attn(q, 64, dst, 64, Tk * 64, dst[half:], 64, Tk * 64, o_hm, 64, B * H, 1, Tk, 0.125)
+    assert torch.equal(o_row, o_hm)
+
+
 def test_greedy_select():
     from tw import ops
     g = torch.Generator().manual_seed(7)
