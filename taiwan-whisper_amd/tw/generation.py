@@ -29,7 +29,7 @@ import torch
 
 from . import ops as F
 
-_XKV_HEAD_MAJOR = os.environ.get("TW_XKV_HEAD_MAJOR", "0") != "0"
+_XKV_HEAD_MAJOR = os.environ.get("TW_XKV_HEAD_MAJOR", "1") != "0"
 
 
 class DecodeSession:
@@ -49,7 +49,7 @@ class DecodeSession:
         # cross-attention K/V head-major (K [B][H][Tk][64] then V): each (clip, head) of the per-step
         # cross-attention reads two contiguous runs instead of 128-B rows 2d apart (tw_kv_head_major; the
         # projection goes through one scratch [B*Tk][2d] block).  TW_XKV_HEAD_MAJOR=0: the projection's own
-        # row-interleaved layout.
+        # row-interleaved layout (A/B runs).
         self.hm = _XKV_HEAD_MAJOR
         if self.hm:
             self.cross_kv = [torch.empty(2 * B * self.H * Tk * 64, dtype=act, device=dev)
