@@ -169,8 +169,19 @@ def run_decode(args, device, rank, world, pg):
     c4 = args.config == "c4"
     # c4: eos suppressed -> every clip decodes exactly --new-tokens (SURVEY.md §8d fixed work)
     m.generation_config = GenerationConfig(suppress_tokens=LARGE_V2_SUPPRESS + ([50257] if c4 else []),
-                                           begin_suppress_tokens=[220, 50257], lang_to_id={"<|zh|>": 50260})
-    kw = dict(language="zh", task="transcribe", max_new_tokens=args.new_tokens)
+                                           begin_suppress_tokens=[220, 50257], lang_to_id={"<|zh|>": 50260},
+                                           max_initial_timestamp_index=50)   # large-v2 generation_config.json
+    if c4:
+        kw = dict(language="zh", task="transcribe", max_new_tokens=args.new_tokens)
+    else:
+        # run_eval.py:637-642 gen_kwargs (generation_max_length 256, :210-211) merged with the long-form
+        # kwargs of :659-665 at their defaults (:148-176: temperature fallback on, compression 1.35, log-prob
+        # -1.0, no-speech 0.6, no conditioning) for every input longer than 30 s (:673-676).
+        # --longform-kwargs none: greedy windows only (the round-2 workload, for comparison).
+        kw = dict(language="zh", task="transcribe", max_length=256)
+        if args.longform_kwargs == "ref":
+            kw.update(condition_on_prev_tokens=False, compression_ratio_threshold=1.35,
+                      temperature=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0), logprob_threshold=-1.0, no_speech_threshold=0.6)
     if c4:
         wavs = [synthetic_audio(args.batch, seed=1000 * rank + i, device=device) for i in range(2)]
 
@@ -194,6 +205,7 @@ def run_decode(args, device, rank, world, pg):
             step(i)
         else:      # warm-up on a 65 s prefix (the kernels and graph capture; not the full recording)
             m.generate(mel_long[:, :, :6500], attention_mask=mask[:, :6500], return_timestamps=True, **kw)
+            trace.clear()
     torch.cuda.synchronize()
     if pg is not None:
         torch.distributed.barrier()
@@ -206,6 +218,7 @@ def run_decode(args, device, rank, world, pg):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    trace_last = list(trace) if not c4 else None
     if pg is not None:
         torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(elapsed.item())
@@ -213,8 +226,8 @@ def run_decode(args, device, rank, world, pg):
         dec_steps = args.steps * (out.shape[1] + 3)                 # prompt prefill (3) + generated columns
         B, t_avg = args.batch, 4 + out.shape[1] / 2
     else:
-        dec_steps = args.steps * sum(len(t["raw"]) + len(t["prompt"]) - 1 for t in trace)
-        B, t_avg = 1, 4 + sum(len(t["raw"]) for t in trace) / max(1, 2 * len(trace))
+        dec_steps = args.steps * sum(len(t["raw"]) + len(t["prompt"]) - 1 for t in trace_last)
+        B, t_avg = 1, 4 + sum(len(t["raw"]) for t in trace_last) / max(1, 2 * len(trace_last))
     ms_dec = elapsed / dec_steps * 1e3
     step_bytes = decode_bytes_per_step(cfg, B, t_avg)
     # dominant kernel (cross-attention over the encoder K/V, the largest per-step read): per-launch HIP
@@ -227,6 +240,7 @@ def run_decode(args, device, rank, world, pg):
         else:
             m.generate(mel_long[:, :, :3000], use_graph=False, return_timestamps=True, language="zh",
                        task="transcribe", max_new_tokens=16)
+            trace.clear()
     ks = timer.summary()
     if rank == 0:
         value = units_per_step * args.steps * world / elapsed
@@ -249,7 +263,7 @@ def run_decode(args, device, rank, world, pg):
             "config": {"workload": (f"c4: whisper-large-v2 batched greedy, {args.batch} x 30 s clips per step, "
                                     f"{args.new_tokens} new tokens" if c4 else
                                     f"c5: whisper-large-v2 long-form, {args.seconds:.0f} s recording, timestamps, "
-                                    f"<= {args.new_tokens} new tokens per window"),
+                                    f"max_length 256 per window, long-form kwargs {args.longform_kwargs}"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch, "parallelism":
                        f"replicas{world}"},
             "decode_steps": dec_steps, "ms_per_decode_step": round(ms_dec, 4),
@@ -258,7 +272,25 @@ def run_decode(args, device, rank, world, pg):
             "cpu_baseline": None,
         }
         if not c4:
-            out_d["windows"] = len(trace)
+            wins = {}
+            for t in trace_last:
+                wins.setdefault((t["b"], t["seek"]), []).append(t)
+            decodes = len(trace_last)
+            skipped = sum(1 for v in wins.values() if v[-1].get("skip"))
+            out_d["windows"] = len(wins)
+            out_d["decodes"] = decodes
+            out_d["fallback_decodes_per_window"] = round((decodes - len(wins)) / max(1, len(wins)), 3)
+            out_d["windows_all_temperatures_failed"] = sum(1 for v in wins.values() if v[-1].get("needs_fallback"))
+            out_d["windows_skipped_no_speech"] = skipped
+            out_d["gate_ms_per_step"] = round(sum(t.get("gate_ms", 0.0) for t in trace_last), 3)
+            out_d["longform_kwargs"] = (
+                "run_eval.py:659-665 defaults: temperature (0.0,0.2,...,1.0), compression_ratio 1.35, "
+                "logprob -1.0, no_speech 0.6, max_length 256" if args.longform_kwargs == "ref" else
+                "none (greedy windows only), max_length 256")
+            if args.longform_kwargs == "ref" and decodes >= 5 * len(wins):
+                out_d["note"] = ("random-init weights: the average log-prob of every window is far below -1.0, so "
+                                 "HF's fallback re-decodes each window at all 6 temperatures (the work of a real "
+                                 "checkpoint is mostly the T=0 pass); --longform-kwargs none times greedy windows")
             out_d["real_time_factor"] = round(elapsed / args.steps / args.seconds, 5)
         print(json.dumps(out_d), flush=True)
     if pg is not None:
@@ -286,6 +318,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--new-tokens", type=int, default=224, help="c4/c5: new tokens per clip / window")
     ap.add_argument("--seconds", type=float, default=1800.0, help="c5: recording length")
+    ap.add_argument("--longform-kwargs", default="ref", choices=["ref", "none"],
+                    help="c5: run_eval.py:659-665 long-form kwargs (ref) or greedy windows only (none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-teacher-fwd", action="store_true")
     args = ap.parse_args()

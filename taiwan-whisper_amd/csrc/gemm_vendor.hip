@@ -81,21 +81,19 @@ int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
                         int N, int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  LtPlan* pl = nullptr;
-  hipblasLtHandle_t h = nullptr;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    h = handle_for(dev);
-    if (!h) return 0;
-    const Key key{dev, M, N, K, lda, ldb, ldc, bias != nullptr, b_trans};
-    auto it = g_plans.find(key);
-    if (it == g_plans.end()) {
-      LtPlan np;
-      np.ok = make_plan(h, np, M, N, K, lda, ldb, ldc, bias != nullptr, b_trans, ws_bytes);
-      it = g_plans.emplace(key, np).first;
-    }
-    pl = &it->second;
+  // the plan's descriptor is shared by every caller of this shape: the bias pointer is written into it and
+  // the matmul enqueued under the lock, so two host threads on one shape cannot swap their bias pointers
+  std::lock_guard<std::mutex> lock(g_mu);
+  hipblasLtHandle_t h = handle_for(dev);
+  if (!h) return 0;
+  const Key key{dev, M, N, K, lda, ldb, ldc, bias != nullptr, b_trans};
+  auto it = g_plans.find(key);
+  if (it == g_plans.end()) {
+    LtPlan np;
+    np.ok = make_plan(h, np, M, N, K, lda, ldb, ldc, bias != nullptr, b_trans, ws_bytes);
+    it = g_plans.emplace(key, np).first;
   }
+  LtPlan* pl = &it->second;
   if (!pl->ok || pl->ws > ws_bytes) return 0;
   if (bias) hipblasLtMatmulDescSetAttribute(pl->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
   const float alpha = 1.f, beta = 0.f;

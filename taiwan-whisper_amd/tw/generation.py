@@ -24,6 +24,7 @@ replayed per token; the host reads the finished flags every 8 steps to stop earl
 from __future__ import annotations
 
 import os
+import time
 
 import torch
 
@@ -54,7 +55,6 @@ class DecodeSession:
         if self.hm:
             self.cross_kv = [torch.empty(2 * B * self.H * Tk * 64, dtype=act, device=dev)
                              for _ in range(cfg.decoder_layers)]
-            self._kv_proj = torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
         else:
             self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
                              for _ in range(cfg.decoder_layers)]
@@ -78,15 +78,19 @@ class DecodeSession:
     def set_encoder(self, enc16):
         """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe)."""
         m, d = self.m, self.d
+        # head-major: the projection goes through one [B*Tk][2d] scratch block that lives only for this call
+        # (3.9 GB at the 512-clip large-v2 batch; the caching allocator reuses it for the next window)
+        proj = torch.empty(self.B * self.Tk, 2 * d, dtype=m.act_dtype, device=m.device) if self.hm else None
         for i, kv in enumerate(self.cross_kv):
             p = f"model.decoder.layers.{i}.encoder_attn"
             wkv = m.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
             bkv = m.wspan(p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
             if self.hm:
-                m._lin(enc16, wkv, bkv, self._kv_proj)
-                F.kv_head_major(self._kv_proj, 2 * d, kv, self.B, self.Tk, self.H)
+                m._lin(enc16, wkv, bkv, proj)
+                F.kv_head_major(proj, 2 * d, kv, self.B, self.Tk, self.H)
             else:
                 m._lin(enc16, wkv, bkv, kv)
+        del proj
 
     def _ln(self, x, name):
         m = self.m
@@ -389,6 +393,8 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     if P >= max_length:
         return torch.empty(B, 0, dtype=torch.int64, device=model.device)
     dec = _Decoder(model, gc, B, Tk, P, max_length, bool(return_timestamps), use_graph)
+    if kw.get("_keep") is not None:          # tests: the decoder (and its device caches) outlive the call
+        kw["_keep"].append(dec)
     return dec.run(enc16, prompt.to(model.device))
 
 
@@ -493,13 +499,15 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                     cand = cand[:k] if pad == eos else cand[:k - 1]
                 needs = False
                 if track or compression_ratio_threshold is not None:
+                    tg = time.perf_counter()          # gate cost: log-prob / no-speech readback + compression ratio
                     avg = float(dec.sel.sum_logp[0]) / max(len(cand), 1) if track else 0.0
                     nsp = float(torch.exp(dec.ns_logp[0])) if ns is not None else 0.0
                     needs, skip = need_fallback(cand, avg, nsp, V, compression_ratio_threshold, logprob_threshold,
                                                 no_speech_threshold)
                     if trace is not None:
                         trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw),
-                                          avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip))
+                                          avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip,
+                                          gate_ms=(time.perf_counter() - tg) * 1e3))
                 elif trace is not None:
                     trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw)))
                 seq, t_acc = raw, temp

@@ -442,7 +442,8 @@ class WhisperForConditionalGeneration:
         student's fp32 stream for both (the fp32 read-modify-write leaves the persistent GEMM's epilogue), on
         the bf16 teacher stream for out_proj only (the plain projection then runs on hipBLASLt; at fc2 the extra
         LN traffic costs what the epilogue saves).  DESIGN.md §5; TW_DEFER_RES=0 disables (A/B runs)."""
-        if not _DEFER_RES or self.act_dtype != torch.bfloat16 or self.config.d_model % 256:
+        # tw_add_layernorm_fwd: D % 256 == 0 and D <= 1280 (every Whisper size), else the residual epilogue
+        if not _DEFER_RES or self.act_dtype != torch.bfloat16 or self.config.d_model % 256 or self.config.d_model > 1280:
             return False
         return self.stream_dtype == torch.float32 or kind == "attn"
 

@@ -25,6 +25,7 @@ Differences, by design or by what this image lacks (each stated where it applies
 from __future__ import annotations
 
 import argparse
+import collections
 import concurrent.futures as cf
 import csv
 import os
@@ -117,23 +118,47 @@ class ChunkTranscriber:
 def transcribe_files(paths: Sequence[str], transcribe: Callable[[Sequence[np.ndarray]], List[List[int]]],
                      decode: Callable[[List[int]], str], chunk_length: float, batch_size: int,
                      read_audio: Callable[[str], Tuple[np.ndarray, int]], num_workers: int = 8,
-                     log: Callable[[str], None] = print) -> Dict[str, Optional[List[dict]]]:
+                     log: Callable[[str], None] = print,
+                     on_done: Optional[Callable[[str, List[dict]], None]] = None,
+                     max_ahead: Optional[int] = None) -> Dict[str, Optional[List[dict]]]:
     """-> {path: rows or None (missing / failed file)}.  Files are decoded on `num_workers` host threads
-    ahead of the GPU; chunks of consecutive files fill batches of `batch_size` across file boundaries."""
+    ahead of the GPU, at most `max_ahead` (default 2 x num_workers) files in flight, so host memory holds a
+    bounded number of decoded waveforms whatever the manifest size; chunks of consecutive files fill
+    batches of `batch_size` across file boundaries.  `on_done(path, rows)` runs as soon as a file's last
+    chunk is transcribed (the reference writes each CSV when its file finishes, initial_inference.py:106-
+    115).  A batch whose transcription or text decoding raises marks every file with a chunk in it as
+    failed (logged, result None, its other chunks dropped) and the run goes on (:116-119)."""
     results: Dict[str, Optional[List[dict]]] = {}
     pending: List[Tuple[str, float, float, np.ndarray]] = []
     counts: Dict[str, int] = {}
     rows: Dict[str, List[dict]] = {}
 
+    def finish(p, r):
+        results[p] = r
+        if on_done is not None and r is not None:
+            on_done(p, r)
+
     def flush(force=False):
         while pending and (force or len(pending) >= batch_size):
             batch = pending[:batch_size]
             del pending[:batch_size]
-            toks = transcribe([c[3] for c in batch])
-            for (p, s, e, _), t in zip(batch, toks):
-                rows[p].append({"start": f"{s:.2f}", "end": f"{e:.2f}", "text": decode(t)})
+            try:
+                toks = transcribe([c[3] for c in batch])
+                texts = [decode(t) for t in toks]
+            except Exception as e:              # noqa: BLE001 -- log the files of the batch and go on
+                bad = list(dict.fromkeys(c[0] for c in batch))
+                for p in bad:
+                    log(f"Failed to transcribe {p}, error: {e}")
+                    rows.pop(p, None)
+                    counts.pop(p, None)
+                    results[p] = None
+                pending[:] = [c for c in pending if c[0] not in set(bad)]
+                continue
+            for (p, s, e, _), t in zip(batch, texts):
+                rows[p].append({"start": f"{s:.2f}", "end": f"{e:.2f}", "text": t})
                 if len(rows[p]) == counts[p]:
-                    results[p] = rows.pop(p)
+                    counts.pop(p)
+                    finish(p, rows.pop(p))
 
     def load(p):
         if not os.path.exists(p):
@@ -144,8 +169,22 @@ def transcribe_files(paths: Sequence[str], transcribe: Callable[[Sequence[np.nda
         except Exception as e:                  # noqa: BLE001 -- the reference logs and skips the file
             return p, None, str(e)
 
+    ahead = max(1, max_ahead if max_ahead is not None else 2 * max(1, num_workers))
     with cf.ThreadPoolExecutor(max(1, num_workers)) as ex:
-        for p, chunks, err in ex.map(load, paths):
+        futs: "collections.deque[cf.Future]" = collections.deque()
+        it = iter(paths)
+
+        def refill():
+            while len(futs) < ahead:
+                try:
+                    futs.append(ex.submit(load, next(it)))
+                except StopIteration:
+                    return
+
+        refill()
+        while futs:
+            p, chunks, err = futs.popleft().result()
+            refill()                            # keep the read-ahead window full while the GPU works
             log(f"Processing: {p}")
             if err == "missing":
                 log(f"File not found: {p}")
@@ -155,11 +194,12 @@ def transcribe_files(paths: Sequence[str], transcribe: Callable[[Sequence[np.nda
                 log(f"Failed to transcribe {p}, error: {err}")
                 results[p] = None
                 continue
-            counts[p], rows[p] = len(chunks), []
             if not chunks:
-                results[p] = rows.pop(p)
+                finish(p, [])
                 continue
+            counts[p], rows[p] = len(chunks), []
             pending.extend((p, s, e, w) for s, e, w in chunks)
+            del chunks
             flush()
         flush(force=True)
     return results
@@ -195,15 +235,14 @@ def main(argv=None):
     tr = ChunkTranscriber(model, args.language, args.max_new_tokens)
     paths = load_dataset(args.dataset_path)[rank::world]
     os.makedirs(args.output_dir, exist_ok=True)
-    res = transcribe_files(paths, tr, decode, args.chunk_length, args.batch_size, read_audio, args.num_workers,
-                           log=(lambda s: print(s, flush=True)) if args.log_progress else (lambda s: None))
-    for p in paths:
-        r = res.get(p)
-        if r is None:
-            continue
+    def write(p, r):
         out = os.path.join(args.output_dir, os.path.splitext(os.path.basename(p))[0] + ".csv")
         save_transcription_to_csv(r, out)
         print(f"Transcription completed: {out}", flush=True)
+
+    res = transcribe_files(paths, tr, decode, args.chunk_length, args.batch_size, read_audio, args.num_workers,
+                           log=(lambda s: print(s, flush=True)) if args.log_progress else (lambda s: None),
+                           on_done=write)
     return res
 
 

@@ -75,3 +75,48 @@ def test_load_dataset(tmp_path):
     m = tmp_path / "m.csv"
     m.write_text("audio_path,duration\n/x/1.flac,3\n/x/2.flac,4\n")
     assert pl.load_dataset(str(m)) == ["/x/1.flac", "/x/2.flac"]
+
+
+def test_transcribe_files_bounded_readahead_and_failures(tmp_path):
+    """the read-ahead is bounded (2 x workers files in flight), each file is reported as soon as
+    its last chunk is done (the reference writes each CSV when its file finishes), and a batch whose
+    transcription raises fails only the files in it (initial_inference.py:116-119)."""
+    import threading
+    import time
+    n_files = 40
+    paths = [f"/virtual/{i}.wav" for i in range(n_files)]
+    lock = threading.Lock()
+    state = {"live": 0, "peak": 0, "consumed": 0}
+
+    def read_audio(p):
+        with lock:
+            state["live"] += 1
+            state["peak"] = max(state["peak"], state["live"] - state["consumed"])
+        time.sleep(0.002)
+        i = int(os.path.basename(p).split(".")[0])
+        return np.full(16000 * (1 + i % 3), i / 100.0, dtype=np.float32), 16000
+
+    done_order = []
+
+    def fake(chunks):
+        state["consumed"] += len({round(float(c[0]) * 100) for c in chunks})
+        ids = [int(round(float(c[0]) * 100)) for c in chunks]
+        if 7 in ids:
+            raise RuntimeError("synthetic GPU error")
+        return [[i] for i in ids]
+    real_exists = os.path.exists
+    try:
+        pl.os.path.exists = lambda p: p.startswith("/virtual/") or real_exists(p)
+        res = pl.transcribe_files(paths, fake, lambda t: str(t[0]), 1, 3, read_audio, num_workers=2,
+                                  log=lambda s: None, on_done=lambda p, r: done_order.append(p))
+    finally:
+        pl.os.path.exists = real_exists
+    # files whose chunks shared the batch with file 7 failed; everything else completed, once, in order
+    failed = [p for p in paths if res[p] is None]
+    assert paths[7] in failed and 0 < len(failed) <= 3
+    assert done_order == [p for p in paths if res[p] is not None]
+    for i, p in enumerate(paths):
+        if res[p] is not None:
+            assert len(res[p]) == 1 + i % 3 and all(r["text"] == str(i) for r in res[p])
+    # read-ahead bound: loads started but not yet consumed never exceed the window (+ the batch in hand)
+    assert state["peak"] <= 2 * 2 + 3
