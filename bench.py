@@ -155,6 +155,20 @@ def decode_bytes_per_step(cfg, B, t_avg, Tk=1500, elem=2):
     return weights + cross + self_kv
 
 
+def _heartbeat(tag, every=30.0):
+    """Print a progress line to stderr every `every` seconds while a long decode runs (the c5 step with the
+    reference's fallback kwargs is minutes long; a silent process looks hung to the GPU-box watchdog)."""
+    import threading
+    t0 = time.time()
+    stop = threading.Event()
+
+    def loop():
+        while not stop.wait(every):
+            print(f"[bench {tag}] running, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=loop, daemon=True).start()
+    return stop
+
+
 def run_decode(args, device, rank, world, pg):
     """c4 (batched greedy pseudo-labelling) and c5 (long-form eval) on large-v2 (random-init bf16:
     the reference runs these in the checkpoint's dtype under its fp16/bf16 flag)."""
@@ -164,7 +178,11 @@ def run_decode(args, device, rank, world, pg):
     from tw.modeling import WhisperForConditionalGeneration, random_init_
     from tw.profiling import KernelTimer
     cfg = WhisperConfig(**MODEL_DIMS["large-v2"])
-    m = random_init_(WhisperForConditionalGeneration(cfg, dtype=torch.bfloat16, device=device), seed=0)
+    hb = _heartbeat(args.config)
+    # --dtype fp16 (default): the reference's decode arithmetic (run_eval.py:99 --dtype float16, :500-509;
+    # run_pseudo_labelling.py:461-463 via run-pseudo-labelling.sh:30); bf16: the autocast-style bf16 model
+    dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    m = random_init_(WhisperForConditionalGeneration(cfg, dtype=dt, device=device), seed=0)
     fe = WhisperFeatureExtractor(device=device)
     c4 = args.config == "c4"
     # c4: eos suppressed -> every clip decodes exactly --new-tokens (SURVEY.md §8d fixed work)
@@ -257,7 +275,7 @@ def run_decode(args, device, rank, world, pg):
                        "long-form transcription speed (audio seconds per wall second)"),
             "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (sines + noise, random-init large-v2 weights)" + (
                 "; eos suppressed -> fixed tokens per clip" if c4 else ""),
             "config": {"workload": (f"c4: whisper-large-v2 batched greedy, {args.batch} x 30 s clips per step, "
@@ -293,6 +311,7 @@ def run_decode(args, device, rank, world, pg):
                                  "checkpoint is mostly the T=0 pass); --longform-kwargs none times greedy windows")
             out_d["real_time_factor"] = round(elapsed / args.steps / args.seconds, 5)
         print(json.dumps(out_d), flush=True)
+    hb.set()
     if pg is not None:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
@@ -318,6 +337,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--new-tokens", type=int, default=224, help="c4/c5: new tokens per clip / window")
     ap.add_argument("--seconds", type=float, default=1800.0, help="c5: recording length")
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"],
+                    help="c4/c5: model dtype (the reference's decode call sites default to float16)")
     ap.add_argument("--longform-kwargs", default="ref", choices=["ref", "none"],
                     help="c5: run_eval.py:659-665 long-form kwargs (ref) or greedy windows only (none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -19,6 +19,11 @@ bf16 stream for bf16 params such as the teacher, `run_distillation.py:1011-1018`
 Attention under amp follows the flash/SDPA recipe: fp32 scores, P = exp(S - max)
 rounded to bf16 for the PV product, normalised by the fp32 row sum, output bf16.
 `amp=False` is the plain fp32 model (the golden-vector pin against HF).
+`half=torch.float16` (with amp=True, stream_bf16=True) is the torch_dtype=float16 model without autocast
+(run_eval.py:99,500-509, run_pseudo_labelling.py:461-463): the same rounding points in fp16 (fp16
+weights, Linear / conv / SDPA outputs, residual stream; LayerNorm and GELU computed in fp32, rounded to
+fp16; P rounded to fp16 for PV), plus the fp16 encoder-layer clamp (HF:409-411).  Pinned to HF fp16 on
+CPU (tests/golden/fp16.npz, tests/test_oracle_golden.py).
 """
 from __future__ import annotations
 
@@ -35,30 +40,34 @@ def _bf(x):
 class Ref:
     """Functional Whisper over an HF-keyed state dict of torch tensors."""
 
-    def __init__(self, cfg: dict, params: dict, amp: bool = False, stream_bf16: bool = False):
+    def __init__(self, cfg: dict, params: dict, amp: bool = False, stream_bf16: bool = False, half=torch.bfloat16):
         self.cfg, self.p, self.amp, self.sbf = cfg, params, amp, stream_bf16
         self.d = cfg["d_model"]
+        self.half = half
+        self.f16 = half == torch.float16
+        self._bf = lambda x: x.to(half).to(torch.float32)       # the 16-bit rounding point
 
     # -- primitives -------------------------------------------------------
     def lin(self, x, w, b=None):
         if self.amp:
-            y = _bf(x) @ _bf(w).t()
+            y = self._bf(x) @ self._bf(w).t()
             if b is not None:
-                y = y + _bf(b)
-            return _bf(y)
+                y = y + self._bf(b)
+            return self._bf(y)
         return F.linear(x, w, b)
 
     def ln(self, x, pfx):
         w, b = self.p[pfx + ".weight"].float(), self.p[pfx + ".bias"].float()
-        return F.layer_norm(x.float(), (self.d,), w, b, 1e-5)
+        y = F.layer_norm(x.float(), (self.d,), w, b, 1e-5)
+        return self._bf(y) if self.f16 else y
 
     def gelu(self, x):
         y = F.gelu(x)
-        return _bf(y) if self.amp else y
+        return self._bf(y) if self.amp else y
 
     def resid(self, r, y):
         out = r + y
-        return _bf(out) if self.sbf else out
+        return self._bf(out) if self.sbf else out
 
     def attn(self, q, k, v, causal):
         """q,k,v [B,H,T,hd] with q already scaled."""
@@ -71,7 +80,7 @@ class Ref:
             m = s.amax(-1, keepdim=True)
             e = torch.exp(s - m)
             l = e.sum(-1, keepdim=True)
-            return _bf((_bf(e) @ v) / l)
+            return self._bf((self._bf(e) @ v) / l)
         return torch.softmax(s, -1) @ v
 
     def mha(self, x, kv, pfx, H, causal):
@@ -98,9 +107,10 @@ class Ref:
         w1, b1 = p["model.encoder.conv1.weight"], p["model.encoder.conv1.bias"]
         w2, b2 = p["model.encoder.conv2.weight"], p["model.encoder.conv2.bias"]
         if self.amp:
-            h = _bf(F.conv1d(_bf(x), _bf(w1), _bf(b1), padding=1))
+            bf = self._bf
+            h = bf(F.conv1d(bf(x), bf(w1), bf(b1), padding=1))
             h = self.gelu(h)
-            h = _bf(F.conv1d(h, _bf(w2), _bf(b2), stride=2, padding=1))
+            h = bf(F.conv1d(h, bf(w2), bf(b2), stride=2, padding=1))
             h = self.gelu(h)
         else:
             h = F.gelu(F.conv1d(x, w1.float(), b1.float(), padding=1))
@@ -112,6 +122,8 @@ class Ref:
             x = self.ln(h, pf + ".self_attn_layer_norm")
             h = self.resid(h, self.mha(x, x, pf + ".self_attn", H, False))
             h = self.resid(h, self.mlp(self.ln(h, pf + ".final_layer_norm"), pf))
+            if self.f16:
+                h = h.clamp(-64504.0, 64504.0).to(torch.float16).float()
         return self.ln(h, "model.encoder.layer_norm")
 
     def decoder(self, ids, enc):

@@ -76,6 +76,12 @@ __device__ __forceinline__ bf16x8 ld_frag(const bf16* base, int64_t ld, int row,
 __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
   return bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
 }
+// P as the 16-bit operand type of the instantiation (bf16 words, or fp16 words for the fp16 path)
+template <bool H>
+__device__ __forceinline__ bf16x8 pack8e(const f32x4& a, const f32x4& b) {
+  return bf16x8{f2e<H>(a[0]), f2e<H>(a[1]), f2e<H>(a[2]), f2e<H>(a[3]),
+                f2e<H>(b[0]), f2e<H>(b[1]), f2e<H>(b[2]), f2e<H>(b[3])};
+}
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
@@ -103,6 +109,9 @@ __device__ __forceinline__ void remap_bh(int& xblk, int& bh) {
 constexpr float NEG_BIG = -1e30f;
 
 // ------------------------------------------------------------------------------------
+// H = false: bf16 Q/K/V/O (autocast); H = true: fp16 (the fp16 decode path: P rounded to fp16 for PV,
+// as SDPA's fp16 flash kernel rounds it)
+template <bool H>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // [2 stages][K, V]
   const int lane = lane_id(), wave = wave_id_uniform();
@@ -172,8 +181,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
       s[kj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        s[kj][0] = MFMA(kf[kj][kk], qf[0][kk], s[kj][0]);
-        s[kj][1] = MFMA(kf[kj][kk], qf[1][kk], s[kj][1]);
+        s[kj][0] = mma16<H>(kf[kj][kk], qf[0][kk], s[kj][0]);
+        s[kj][1] = mma16<H>(kf[kj][kk], qf[1][kk], s[kj][1]);
       }
     }
     // online softmax (log2 domain), per query column.  Masking only on boundary tiles
@@ -237,12 +246,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     // O^T += V^T P^T
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 p0 = pack8(s[2 * ss][0], s[2 * ss + 1][0]);
-      const bf16x8 p1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
+      const bf16x8 p0 = pack8e<H>(s[2 * ss][0], s[2 * ss + 1][0]);
+      const bf16x8 p1 = pack8e<H>(s[2 * ss][1], s[2 * ss + 1][1]);
 #pragma unroll
       for (int hj = 0; hj < 4; ++hj) {
-        o[hj][0] = MFMA(vf[hj][ss], p0, o[hj][0]);
-        o[hj][1] = MFMA(vf[hj][ss], p1, o[hj][1]);
+        o[hj][0] = mma16<H>(vf[hj][ss], p0, o[hj][0]);
+        o[hj][1] = mma16<H>(vf[hj][ss], p1, o[hj][1]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
 #pragma unroll
       for (int hj = 0; hj < 4; ++hj) {
         const f32x4 v = o[hj][qi] * inv;
-        *(bf16x4*)(Ob + hj * 16 + 4 * g) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        *(bf16x4*)(Ob + hj * 16 + 4 * g) = bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
       }
       if (g == 0 && p.lse) p.lse[(int64_t)bh * p.Tq + q] = (m[qi] + log2f(lt)) / LOG2E;
     }
@@ -802,8 +811,26 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
   } else if (variant == 8) {
     hipLaunchKernelGGL(attn_fwd32_kernel<8>, dim3((Tq + 255) / 256, B * H), dim3(512), 0, stream, p);
   } else {
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   }
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+// fp16 Q/K/V/O (HF Whisper with torch_dtype=float16: SDPA over fp16 projections, run_eval.py:99,500-509)
+extern "C" int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
+                               void* O, int64_t ldo, float* lse, int B, int H, int Tq, int Tk, int head_dim, int causal,
+                               float scale, hipStream_t stream) {
+  if (head_dim != 64) return TW_EUNSUPPORTED;
+  if (B <= 0 || Tq <= 0 || Tk <= 0) return TW_OK;
+  if (!check_common(Q, K, V, ldq, ldk, ldv) || (ldo & 3)) return TW_EINVAL;
+  if (causal && Tq > Tk) return TW_EINVAL;
+  AttnP p = {};
+  p.Q = (const bf16*)Q; p.K = (const bf16*)K; p.V = (const bf16*)V; p.O = (bf16*)O; p.lse = lse;
+  p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
+  p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
+  p.scale = scale; p.scale_log2 = scale * LOG2E;
+  hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -24,11 +24,45 @@ typedef __attribute__((address_space(3))) void lds_void;
   } while (0)
 
 // dtype codes shared with the host side
-enum { TW_F32 = 0, TW_BF16 = 1 };
+enum { TW_F32 = 0, TW_BF16 = 1, TW_F16 = 2 };
+
+typedef _Float16 f16;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 __device__ __forceinline__ float rbf(float x) { return (float)(bf16)x; }   // round-trip through bf16 (RNE)
+
+// ---- 16-bit operand codec of the MFMA kernels.  Their operands and 16-bit outputs are moved as raw 16-bit
+// words (typed `bf16` in the kernels: loads, LDS images, fragments); H selects what the words hold:
+// H = false: bf16 (the CUDA-autocast path), H = true: IEEE fp16 (the reference's torch_dtype=float16
+// decode path, run_eval.py:99,500-509 / run_pseudo_labelling.py:461-463).  Rounding is RNE either way.
+template <bool H>
+__device__ __forceinline__ float e2f(bf16 x) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, x);
+  else return (float)x;
+}
+template <bool H>
+__device__ __forceinline__ bf16 f2e(float x) {
+  if constexpr (H) return __builtin_bit_cast(bf16, (_Float16)x);
+  else return (bf16)x;
+}
+template <bool H>
+__device__ __forceinline__ float rnd(float x) { return e2f<H>(f2e<H>(x)); }
+// v_mfma_f32_16x16x32_{bf16,f16}: A, B = 8 16-bit words per lane, fp32 accumulate
+template <bool H>
+__device__ __forceinline__ f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// fp16 saturation of HF WhisperEncoderLayer (modeling_whisper.py:409-411: clamp to finfo(fp16).max - 1000 after
+// the MLP residual when the stream is fp16); applied to the fp16-rounded value, so +-inf -> the bound too
+__device__ __forceinline__ float clamp_f16_stream(float x) {
+  return fminf(fmaxf(x, -64504.0f), 64504.0f);
+}
 
 // 8 consecutive elements of a bf16 / fp32 row as fp32 (16-B / 2 x 16-B vector loads; the caller
 // guarantees alignment), and the inverse store
@@ -51,13 +85,32 @@ __device__ __forceinline__ void store8(float* p, const float* v) {
   *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
   *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
+__device__ __forceinline__ void load8(const f16* p, float* o) {
+  const f16x8 v = *(const f16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (float)v[j];
+}
+__device__ __forceinline__ void store8(f16* p, const float* v) {
+  f16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (_Float16)v[j];
+  *(f16x8*)p = o;
+}
 __device__ __forceinline__ float to_f32(bf16 x) { return bf2f(x); }
+__device__ __forceinline__ float to_f32(f16 x) { return (float)x; }
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ void from_f32(bf16& d, float x) { d = f2bf(x); }
+__device__ __forceinline__ void from_f32(f16& d, float x) { d = (_Float16)x; }
 __device__ __forceinline__ void from_f32(float& d, float x) { d = x; }
 
 __device__ __forceinline__ float ld_as_f32(const void* p, int dtype, int64_t i) {
-  return dtype == TW_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+  return dtype == TW_BF16 ? (float)((const bf16*)p)[i]
+       : dtype == TW_F16  ? (float)((const f16*)p)[i] : ((const float*)p)[i];
+}
+__device__ __forceinline__ void st_from_f32(void* p, int dtype, int64_t i, float v) {
+  if (dtype == TW_BF16) ((bf16*)p)[i] = f2bf(v);
+  else if (dtype == TW_F16) ((f16*)p)[i] = (_Float16)v;
+  else ((float*)p)[i] = v;
 }
 
 // erf, branch-free (Abramowitz & Stegun 7.1.26: |error| <= 1.5e-7 absolute, ~14 VALU, no

@@ -648,8 +648,7 @@ __global__ void embed_step_kernel(const int64_t* __restrict__ ids, const void* _
   const int64_t t = *t_dev;
   for (int e = threadIdx.x; e < D; e += blockDim.x) {
     const float s = ld_as_f32(tok, tok_dtype, id * D + e) + ld_as_f32(pos, pos_dtype, t * D + e);
-    if (out_dtype == TW_BF16) ((bf16*)out)[(int64_t)b * D + e] = f2bf(s);
-    else ((float*)out)[(int64_t)b * D + e] = s;
+    st_from_f32(out, out_dtype, (int64_t)b * D + e, s);
   }
 }
 
@@ -677,6 +676,7 @@ int sel_vec(const void* logits, int64_t ld, int V) {
 #define TW_LAUNCH_DT(dt, K, grid, block, ...)                                              \
   do {                                                                                      \
     if ((dt) == TW_BF16) hipLaunchKernelGGL(K<bf16>, grid, block, 0, stream, __VA_ARGS__);   \
+    else if ((dt) == TW_F16) hipLaunchKernelGGL(K<f16>, grid, block, 0, stream, __VA_ARGS__);  \
     else if ((dt) == TW_F32) hipLaunchKernelGGL(K<float>, grid, block, 0, stream, __VA_ARGS__); \
     else return TW_EUNSUPPORTED;                                                            \
   } while (0)
@@ -760,6 +760,8 @@ extern "C" int tw_token_logprob(const void* logits, int64_t ld, int logits_dtype
   if (V <= 0 || ld < V || token < 0 || token >= V || !out) return TW_EINVAL;
   if (logits_dtype == TW_BF16)
     hipLaunchKernelGGL(token_logprob_kernel<bf16>, dim3(B), dim3(256), 0, stream, (const bf16*)logits, ld, V, token, out);
+  else if (logits_dtype == TW_F16)
+    hipLaunchKernelGGL(token_logprob_kernel<f16>, dim3(B), dim3(256), 0, stream, (const f16*)logits, ld, V, token, out);
   else if (logits_dtype == TW_F32)
     hipLaunchKernelGGL(token_logprob_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)logits, ld, V, token,
                        out);
@@ -806,7 +808,7 @@ extern "C" int tw_kv_head_major(const void* src, int64_t ld, void* dst, int B, i
   const int64_t rows = (int64_t)B * Tk;
   const int64_t nvec = rows * (2 * 64 * H) / (w + 1);
   const dim3 grid((unsigned)std::min<int64_t>((nvec + 255) / 256, 16384));
-  if (dtype == TW_BF16)
+  if (dtype == TW_BF16 || dtype == TW_F16)
     hipLaunchKernelGGL(kv_head_major_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)src, ld, (bf16*)dst, Tk, H,
                        rows);
   else if (dtype == TW_F32)
@@ -824,7 +826,7 @@ extern "C" int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_
   const int w = dtype == TW_F32 ? 3 : 7;          // 16-B vectors: 4 fp32 / 8 bf16
   if (!t_dev || (n & w) || (ld_src & w) || (ld_row & w) || (sb & w) || (((uintptr_t)src | (uintptr_t)cache) & 15))
     return TW_EINVAL;
-  if (dtype == TW_BF16)
+  if (dtype == TW_BF16 || dtype == TW_F16)
     hipLaunchKernelGGL(kv_append_kernel<bf16>, dim3((n / 8 + 255) / 256, B), dim3(256), 0, stream, (const bf16*)src,
                        ld_src, (bf16*)cache, ld_row, sb, n, t_dev);
   else if (dtype == TW_F32)

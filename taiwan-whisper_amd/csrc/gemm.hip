@@ -26,7 +26,7 @@ using namespace twg;
 // STAGES-deep LDS ring, prefetch distance STAGES-1; waits are counted (vmcnt = loads of the
 // stages allowed to stay in flight) and the barrier is a raw s_barrier, so in-flight LDS-DMA
 // survives it (a __syncthreads() would drain vmcnt(0)).
-template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
+template <bool H, bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
   constexpr int NW = WM * WN;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
         for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
           for (int ni = 0; ni < FN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][ni], a[kk][mi], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = mma16<H>(b[kk][ni], a[kk][mi], acc[mi][ni]);
     } else {
       if (kt + PD < nk) stage(nxt, kt + PD);
 #pragma unroll
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
         for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
           for (int ni = 0; ni < FN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ni], a[mi], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = mma16<H>(b[ni], a[mi], acc[mi][ni]);
       }
     }
     // stage kt+1 must have landed; stages kt+2 .. kt+PD (when issued) may stay in flight
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
     __builtin_amdgcn_s_barrier();
   }
 
-  epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
+  epilogue<H, BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -176,7 +176,7 @@ __device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_
 // prio 1 around each MFMA phase; 1 = the same with static prio 1 for the trailing wave row
 // (waves 4-7), no flips; 2 = diagnostic: every MFMA phase issued twice (wrong results; measures
 // the fixed per-phase cost); 4 = two 32-MFMA phases per K-tile (default: +4-8 % main loop)
-template <int PRIO>
+template <bool H, int PRIO>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_REGION];
   const int lane = lane_id();
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni)
             acc[qm * 4 + mi][qq * 2 + ni] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[qq][kk][ni], a[kk][mi], acc[qm * 4 + mi][qq * 2 + ni], 0, 0, 0);
+                mma16<H>(bq[qq][kk][ni], a[kk][mi], acc[qm * 4 + mi][qq * 2 + ni]);
     __builtin_amdgcn_s_setprio(0);
     sync();
   };
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
           acc[qm * 4 + mi][qn * 2 + ni] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[kk][ni], a[kk][mi], acc[qm * 4 + mi][qn * 2 + ni], 0, 0, 0);
+              mma16<H>(bb[kk][ni], a[kk][mi], acc[qm * 4 + mi][qn * 2 + ni]);
     if constexpr (PRIO == 0 || PRIO == 2) __builtin_amdgcn_s_setprio(0);
     sync();
   };
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       {
         int m0, n0, bz;
         pp_tile(p, ti, m0, n0, bz);
-        epilogue<256, 256, 2, 4>(p, acc, m0, n0, wm, wn, lane, bz);
+        epilogue<H, 256, 256, 2, 4>(p, acc, m0, n0, wm, wn, lane, bz);
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -368,11 +368,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 }
 
 
-template <bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
+template <bool H, bool AT, bool BT, int BM, int BN, int WM, int WN, int STAGES>
 void launch(GemmP p, int batch, hipStream_t stream) {
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_mn = p.tiles_n * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_kernel<AT, BT, BM, BN, WM, WN, STAGES>), dim3(p.tiles_mn, 1, batch), dim3(WM * WN * 64), 0,
+  hipLaunchKernelGGL((gemm_kernel<H, AT, BT, BM, BN, WM, WN, STAGES>), dim3(p.tiles_mn, 1, batch), dim3(WM * WN * 64), 0,
                      stream, p);
 }
 
@@ -384,32 +384,35 @@ void launch(GemmP p, int batch, hipStream_t stream) {
 // operands, the 4 wave partials summed through LDS, then the per-element epilogue (every flag).
 // ---------------------------------------------------------------------------------------------
 // the epilogue value of C[m][n] (writes the GELU pre-activation to aux on the way), before the store
+template <bool H>
 __device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v) {
   const int flags = p.flags;
   v *= p.alpha;
-  if (flags & F_BIAS) v += bf2f(p.bias[n]);
-  if (flags & F_ROUND) v = rbf(v);
-  if (flags & F_DGELU) v = rbf(v * gelu_erf_grad(bf2f(p.aux[(int64_t)m * p.ldaux + n])));
+  if (flags & F_BIAS) v += e2f<H>(p.bias[n]);
+  if (flags & F_ROUND) v = rnd<H>(v);
+  if (flags & F_DGELU) v = rnd<H>(v * gelu_erf_grad(e2f<H>(p.aux[(int64_t)m * p.ldaux + n])));
   if (flags & F_GELU) {
-    if (flags & F_AUX_OUT) p.aux[(int64_t)m * p.ldaux + n] = f2bf(v);
-    v = rbf(gelu_erf(v));
+    if (flags & F_AUX_OUT) p.aux[(int64_t)m * p.ldaux + n] = f2e<H>(v);
+    v = rnd<H>(gelu_erf(v));
   }
   if (flags & F_RES) {
     const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
-    v += ld_as_f32(p.res, p.res_dtype, (int64_t)mr * p.ldr + n);
+    v += ld16_as_f32<H>(p.res, p.res_dtype, (int64_t)mr * p.ldr + n);
   }
-  if (flags & F_ACCUM) v += ld_as_f32(p.C, p.c_dtype, (int64_t)m * p.ldc + n);
+  if (flags & F_ACCUM) v += ld16_as_f32<H>(p.C, p.c_dtype, (int64_t)m * p.ldc + n);
+  if (flags & F_CLAMP16) v = clamp_f16_stream(rnd<H>(v));
   return v;
 }
 
+template <bool H>
 __device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float v) {
-  v = epi_value(p, m, n, v);
+  v = epi_value<H>(p, m, n, v);
   const int64_t co = (int64_t)m * p.ldc + n;
-  if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2bf(v);
+  if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
   else ((float*)p.C)[co] = v;
 }
 
-template <int MF>
+template <bool H, int MF>
 __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
   __shared__ float part[4][MF * 16][17];
   const int lane = lane_id(), wave = wave_id_uniform();
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
     for (int j = 0; j < D; ++j)
 #pragma unroll
       for (int i = 0; i < MF; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[buf][j], ab[buf][j][i], acc[i], 0, 0, 0);
+        acc[i] = mma16<H>(wb[buf][j], ab[buf][j][i], acc[i]);
   };
   if (k_beg < k_end) {
     load_group(0, k_beg);
@@ -483,23 +486,25 @@ __global__ __launch_bounds__(256, 1) void gemm_skinny_kernel(GemmP p) {
     if (m < p.M && n < p.N) {
       const float v = part[0][ml][c] + part[1][ml][c] + part[2][ml][c] + part[3][ml][c];
       if (p.ws) p.ws[((int64_t)blockIdx.y * p.M + m) * p.N + n] = v;
-      else epi_element(p, m, n, v);
+      else epi_element<H>(p, m, n, v);
     }
   }
 }
 
 // sum of the split-K partials of the skinny kernel (in chunk order) + the full epilogue
+template <bool H>
 __global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmP p, int S) {
   const int64_t total = (int64_t)p.M * p.N;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     float v = p.ws[i];
     for (int s = 1; s < S; ++s) v += p.ws[s * total + i];
-    epi_element(p, (int)(i / p.N), (int)(i % p.N), v);
+    epi_element<H>(p, (int)(i / p.N), (int)(i % p.N), v);
   }
 }
 
 // the same, 4 consecutive columns per thread (N % 4 == 0, ldc / ws rows 16-B aligned): the split-K tail
 // of the mid-sized forward GEMMs
+template <bool H>
 __global__ __launch_bounds__(256) void sk_reduce_kernel(GemmP p, int S) {
   const int n4 = p.N >> 2;
   const int64_t total = (int64_t)p.M * p.N, work = (int64_t)p.M * n4;
@@ -510,9 +515,10 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(GemmP p, int S) {
     for (int s = 1; s < S; ++s) a += *(const f32x4*)(w + s * total);
     float v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = epi_value(p, m, n + r, a[r]);
+    for (int r = 0; r < 4; ++r) v[r] = epi_value<H>(p, m, n + r, a[r]);
     const int64_t co = (int64_t)m * p.ldc + n;
-    if (p.c_dtype == TW_BF16) *(bf16x4*)((bf16*)p.C + co) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    if (p.c_dtype == TW_BF16)
+      *(bf16x4*)((bf16*)p.C + co) = bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
     else *(f32x4*)((float*)p.C + co) = f32x4{v[0], v[1], v[2], v[3]};
   }
 }
@@ -537,7 +543,7 @@ struct GemvKV {
   const int* t;
 };
 
-template <int MR, int CPW, int PRE>
+template <bool H, int MR, int CPW, int PRE>
 __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                    float eps, GemvKV kv) {
   extern __shared__ __attribute__((aligned(16))) char gemv_smem[];
@@ -570,7 +576,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
       for (int c = 0; c < nch; ++c) {
         const bf16x8 t = *(const bf16x8*)(xr + (c * 32 + hl) * 8);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) s += bf2f(t[q]);
+        for (int q = 0; q < 8; ++q) s += e2f<H>(t[q]);
       }
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -579,7 +585,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
       for (int c = 0; c < nch; ++c) {
         const bf16x8 t = *(const bf16x8*)(xr + (c * 32 + hl) * 8);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { const float d = bf2f(t[q]) - mean; ss += d * d; }
+        for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[q]) - mean; ss += d * d; }
       }
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
@@ -592,12 +598,12 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
           const f32x4 b0 = *(const f32x4*)(lnb + e), b1 = *(const f32x4*)(lnb + e + 4);
           float v[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = bf2f(t[q]);
+          for (int q = 0; q < 8; ++q) v[q] = e2f<H>(t[q]);
           bf16x8 o;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            o[q] = f2bf((v[q] - mean) * rstd * w0[q] + b0[q]);
-            o[q + 4] = f2bf((v[q + 4] - mean) * rstd * w1[q] + b1[q]);
+            o[q] = f2e<H>((v[q] - mean) * rstd * w0[q] + b0[q]);
+            o[q + 4] = f2e<H>((v[q + 4] - mean) * rstd * w1[q] + b1[q]);
           }
           *(bf16x8*)(dst + e) = o;
         }
@@ -624,7 +630,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
 #pragma unroll
         for (int c = 0; c < CPW; ++c)
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(bf2f(wpre[c][u][q]), bf2f(a8[q]), acc[c][r]);
+          for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(e2f<H>(wpre[c][u][q]), e2f<H>(a8[q]), acc[c][r]);
       }
     }
   }
@@ -637,7 +643,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
       for (int r = 0; r < MR; ++r) {
         const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + k0);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(bf2f(w8[q]), bf2f(a8[q]), acc[c][r]);
+        for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(e2f<H>(w8[q]), e2f<H>(a8[q]), acc[c][r]);
       }
     }
   }
@@ -653,13 +659,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
       for (int r = 0; r < MR; ++r) {
         const int n = n0 + c;
         if (r < p.M && n < p.N) {
-          const float v = epi_value(p, r, n, acc[c][r]);
+          const float v = epi_value<H>(p, r, n, acc[c][r]);
           const int64_t co = (int64_t)r * p.ldc + n;
-          if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2bf(v);
+          if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
           else ((float*)p.C)[co] = v;
           if (kv.cache && n >= kv.col0) {
             const int64_t ko = r * kv.sb + t * kv.ld + (n - kv.col0);
-            if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2bf(v);
+            if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2e<H>(v);
             else ((float*)kv.cache)[ko] = v;
           }
         }
@@ -686,16 +692,17 @@ int skinny_row_blocks(int M) {
   return (env && M > R) ? (M + R - 1) / R : 1;
 }
 
+template <bool H>
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
   const int zb = skinny_row_blocks(p.M);
   const dim3 grid((p.N + 15) / 16, S, zb);
   const int mf = zb > 1 ? skinny_block_rows() / 16 : (p.M + 15) / 16;
   switch (mf) {
-    case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, stream, p); break;
-    case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, stream, p); break;
+    case 1: hipLaunchKernelGGL((gemm_skinny_kernel<H, 1>), grid, dim3(256), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((gemm_skinny_kernel<H, 2>), grid, dim3(256), 0, stream, p); break;
     case 3:
-    case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(256), 0, stream, p); break;
-    default: hipLaunchKernelGGL(gemm_skinny_kernel<8>, grid, dim3(256), 0, stream, p); break;
+    case 4: hipLaunchKernelGGL((gemm_skinny_kernel<H, 4>), grid, dim3(256), 0, stream, p); break;
+    default: hipLaunchKernelGGL((gemm_skinny_kernel<H, 8>), grid, dim3(256), 0, stream, p); break;
   }
 }
 
@@ -717,15 +724,17 @@ int pick_epilogue(const GemmP& p, int batch) {
     const bool x8 = (p.ldaux % 8) == 0 && (batch == 1 || (p.sAux % 8) == 0) && a16(p.aux);
     return x8 ? EPI_GELU_AUX : EPI_GENERIC;
   }
-  if ((f & ~(F_BIAS | F_ROUND)) == F_RES && p.res_mod == 0 && p.res_dtype == p.c_dtype) {
+  if ((f & ~(F_BIAS | F_ROUND | F_CLAMP16)) == F_RES && p.res_mod == 0 && p.res_dtype == p.c_dtype) {
     if (p.c_dtype == TW_BF16 && c8 && (p.ldr % 8) == 0 && (batch == 1 || (p.sR % 8) == 0) && a16(p.res))
       return EPI_RES_BF16;
+    if (f & F_CLAMP16) return EPI_GENERIC;
     if (p.c_dtype == TW_F32 && c4 && (p.ldr % 4) == 0 && (batch == 1 || (p.sR % 4) == 0) && a16(p.res))
       return EPI_RES_F32;
   }
   return EPI_GENERIC;
 }
 
+template <bool H>
 void launch_pp(GemmP p, int batch, hipStream_t stream) {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -745,13 +754,13 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
     return e ? atoi(e) : -1;
   }();
   switch (env_variant >= 0 ? env_variant : (p.flags >> 15) & 7) {
-    case 1: hipLaunchKernelGGL(gemm_pp_kernel<0>, dim3(grid), dim3(512), 0, stream, p); break;
-    case 2: hipLaunchKernelGGL(gemm_pp_kernel<2>, dim3(grid), dim3(512), 0, stream, p); break;
-    case 3: hipLaunchKernelGGL(gemm_pp_kernel<1>, dim3(grid), dim3(512), 0, stream, p); break;
-    case 5: hipLaunchKernelGGL(gemm_pp_kernel<5>, dim3(grid), dim3(512), 0, stream, p); break;
-    case 6: hipLaunchKernelGGL(gemm_pp_kernel<6>, dim3(grid), dim3(512), 0, stream, p); break;
-    case 7: hipLaunchKernelGGL(gemm_pp_kernel<7>, dim3(grid), dim3(512), 0, stream, p); break;
-    default: hipLaunchKernelGGL(gemm_pp_kernel<4>, dim3(grid), dim3(512), 0, stream, p); break;
+    case 1: hipLaunchKernelGGL((gemm_pp_kernel<H, 0>), dim3(grid), dim3(512), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((gemm_pp_kernel<H, 2>), dim3(grid), dim3(512), 0, stream, p); break;
+    case 3: hipLaunchKernelGGL((gemm_pp_kernel<H, 1>), dim3(grid), dim3(512), 0, stream, p); break;
+    case 5: hipLaunchKernelGGL((gemm_pp_kernel<H, 5>), dim3(grid), dim3(512), 0, stream, p); break;
+    case 6: hipLaunchKernelGGL((gemm_pp_kernel<H, 6>), dim3(grid), dim3(512), 0, stream, p); break;
+    case 7: hipLaunchKernelGGL((gemm_pp_kernel<H, 7>), dim3(grid), dim3(512), 0, stream, p); break;
+    default: hipLaunchKernelGGL((gemm_pp_kernel<H, 4>), dim3(grid), dim3(512), 0, stream, p); break;
   }
 }
 
@@ -827,13 +836,13 @@ int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
   return 0;
 }
 
-template <bool AT, bool BT>
+template <bool H, bool AT, bool BT>
 void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
-  if (tile == 2562 && !AT && !BT) launch_pp(p, batch, stream);
-  else if (tile == 256) launch<AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
-  else if (tile == 2561) launch<AT, BT, 256, 128, 4, 2, 3>(p, batch, stream);
-  else if (tile == 2563) launch<AT, BT, 256, 128, 4, 2, 2>(p, batch, stream);
-  else launch<AT, BT, 128, 128, 2, 2, 2>(p, batch, stream);
+  if (tile == 2562 && !AT && !BT) launch_pp<H>(p, batch, stream);
+  else if (tile == 256) launch<H, AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
+  else if (tile == 2561) launch<H, AT, BT, 256, 128, 4, 2, 3>(p, batch, stream);
+  else if (tile == 2563) launch<H, AT, BT, 256, 128, 4, 2, 2>(p, batch, stream);
+  else launch<H, AT, BT, 128, 128, 2, 2, 2>(p, batch, stream);
 }
 
 int pp_grid_cus() {
@@ -879,6 +888,7 @@ int sk_tail_plan(const GemmP& p, int batch, int& m_dp) {
   return best;
 }
 
+template <bool H>
 int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
   const int Mt = p.M - m_dp * 256;
   const size_t bytes = (size_t)S * Mt * p.N * sizeof(float);
@@ -887,7 +897,7 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
   if (m_dp > 0) {
     GemmP d = p;                                       // whole rounds: the unsplit kernel
     d.M = m_dp * 256;
-    launch_pp(d, 1, stream);
+    launch_pp<H>(d, 1, stream);
     TW_CHECK_LAUNCH();
   }
   GemmP q = p;                                         // tail rows: S K-chunks -> fp32 partials
@@ -901,7 +911,7 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
   q.alpha = 1.f; q.flags = 0; q.bias = nullptr; q.res = nullptr; q.aux = nullptr; q.ws = nullptr;
   q.group_m = 1;
   q.epi = pick_epilogue(q, S);
-  launch_pp(q, S, stream);
+  launch_pp<H>(q, S, stream);
   TW_CHECK_LAUNCH();
   GemmP r = p;                                         // ordered chunk sum + the full epilogue
   const int csz = p.c_dtype == TW_BF16 ? 2 : 4;
@@ -911,7 +921,7 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
   r.M = Mt;
   r.ws = ws;
   const int64_t work = (int64_t)Mt * (p.N / 4);
-  hipLaunchKernelGGL(sk_reduce_kernel, dim3((int)std::min<int64_t>((work + 255) / 256, 4096)), dim3(256), 0,
+  hipLaunchKernelGGL(sk_reduce_kernel<H>, dim3((int)std::min<int64_t>((work + 255) / 256, 4096)), dim3(256), 0,
                      stream, r, S);
   TW_CHECK_LAUNCH();
   return 1;
@@ -941,12 +951,25 @@ extern "C" int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, in
           !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) ? 1 : 0;
 }
 
-extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
-                            void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
-                            int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
-                            const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
-                            void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
+namespace {
+
+// H = false: tw_gemm_bf16; H = true: tw_gemm_f16 (forward products only: K-major A and B)
+template <bool H>
+int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans, void* C, int64_t ldc,
+             int c_dtype, int M, int N, int K, int batch, int64_t sA, int64_t sB, int64_t sC, float alpha,
+             const void* bias, const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod, void* aux,
+             int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return TW_OK;
+  if (H) {
+    if (a_trans || b_trans) return TW_EUNSUPPORTED;
+    if ((c_dtype != TW_F32 && c_dtype != TW_F16) || ((flags & F_RES) && res_dtype != TW_F32 && res_dtype != TW_F16))
+      return TW_EUNSUPPORTED;
+    // inside the kernels the 16-bit code means "the operand type" (gemm_impl.h)
+    if (c_dtype == TW_F16) c_dtype = TW_BF16;
+    if (res_dtype == TW_F16) res_dtype = TW_BF16;
+  } else if (flags & F_CLAMP16) {
+    return TW_EINVAL;
+  }
   if (K <= 0) return TW_EINVAL;
   if ((!a_trans || !b_trans) && (K % 8) != 0) return TW_EINVAL;  // 16-B k-chunks of K-major operands
   if (a_trans && (M % 8) != 0) return TW_EINVAL;                // 16-B column chunks
@@ -957,6 +980,7 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
   if ((flags & F_RES) && !res) return TW_EINVAL;
   if ((flags & (F_AUX_OUT | F_DGELU)) && !aux) return TW_EINVAL;
   if (c_dtype != TW_F32 && c_dtype != TW_BF16) return TW_EUNSUPPORTED;
+  if (res_dtype != TW_F32 && res_dtype != TW_BF16) res_dtype = TW_F32;   // unused without F_RES
   GemmP p;
   p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
@@ -1011,18 +1035,18 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
     void* ws = S > 1 ? splitk_workspace(stream, (size_t)S * M * N * sizeof(float)) : nullptr;
     if (ws) {
       p.ws = (float*)ws;
-      launch_skinny(p, stream, S);
+      launch_skinny<H>(p, stream, S);
       TW_CHECK_LAUNCH();
       const int64_t total = (int64_t)M * N;
-      hipLaunchKernelGGL(skinny_reduce_kernel, dim3((int)std::min<int64_t>((total + 255) / 256, 2048)), dim3(256), 0,
+      hipLaunchKernelGGL(skinny_reduce_kernel<H>, dim3((int)std::min<int64_t>((total + 255) / 256, 2048)), dim3(256), 0,
                          stream, p, S);
     } else {
-      launch_skinny(p, stream);
+      launch_skinny<H>(p, stream);
     }
     TW_CHECK_LAUNCH();
     return TW_OK;
   }
-  if (!(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
+  if (!H && !(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
     const int S = splitk_factor(p, batch, a_trans, b_trans);
     const size_t bytes = (size_t)S * M * N * sizeof(float);
     void* ws = (S > 0 && bytes <= ((size_t)1 << 30)) ? splitk_workspace(stream, bytes) : nullptr;
@@ -1035,7 +1059,7 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
       q.C = ws; q.ldc = N; q.sC = (int64_t)M * N; q.c_dtype = TW_F32;
       q.alpha = 1.f; q.flags = 0; q.bias = nullptr; q.res = nullptr; q.aux = nullptr;
       q.epi = pick_epilogue(q, S);
-      launch<true, true, 128, 128, 2, 2, 2>(q, S, stream);
+      launch<false, true, true, 128, 128, 2, 2, 2>(q, S, stream);
       TW_CHECK_LAUNCH();
       const int64_t work = (int64_t)M * (N / 4);
       const int grid = (int)std::min<int64_t>((work + 255) / 256, 4096);
@@ -1047,7 +1071,7 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
     }
   }
   // plain forward projections (bias + bf16 out, K <= 2048, M >= 4096): hipBLASLt (csrc/gemm_vendor.hip)
-  if (tw_gemm_backend(M, N, K, a_trans, b_trans, c_dtype, batch, alpha, flags) == 1) {
+  if (!H && tw_gemm_backend(M, N, K, a_trans, b_trans, c_dtype, batch, alpha, flags) == 1) {
     const size_t ws_bytes = (size_t)64 << 20;
     void* ws = splitk_workspace(stream, ws_bytes);
     if (ws) {
@@ -1070,22 +1094,34 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
       !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
     int m_dp = 0;
     const int S = sk_tail_plan(p, batch, m_dp);
-    if (S > 0 && launch_sk_tail(p, S, m_dp, stream)) return TW_OK;
+    if (S > 0 && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
   }
-  if (!a_trans && !b_trans) dispatch<false, false>(p, batch, stream, tile);
-  else if (!a_trans && b_trans) dispatch<false, true>(p, batch, stream, tile);
-  else if (a_trans && !b_trans) dispatch<true, false>(p, batch, stream, tile);
-  else dispatch<true, true>(p, batch, stream, tile);
+  if constexpr (H) {
+    dispatch<true, false, false>(p, batch, stream, tile);
+  } else {
+    if (!a_trans && !b_trans) dispatch<false, false, false>(p, batch, stream, tile);
+    else if (!a_trans && b_trans) dispatch<false, false, true>(p, batch, stream, tile);
+    else if (a_trans && !b_trans) dispatch<false, true, false>(p, batch, stream, tile);
+    else dispatch<false, true, true>(p, batch, stream, tile);
+  }
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
 
-extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
-                            int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
-                            const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
-                            void* kv_cache, int64_t kv_sb, int64_t kv_ld, int kv_col0, const int* t_dev,
-                            hipStream_t stream) {
+template <bool H>
+int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W, int64_t ldw,
+             void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias, const void* res, int64_t ldr,
+             int res_dtype, void* aux, int64_t ldaux, int flags, void* kv_cache, int64_t kv_sb, int64_t kv_ld,
+             int kv_col0, const int* t_dev, hipStream_t stream) {
   if (M <= 0 || N <= 0) return TW_OK;
+  if (H) {
+    if ((c_dtype != TW_F32 && c_dtype != TW_F16) || ((flags & F_RES) && res_dtype != TW_F32 && res_dtype != TW_F16))
+      return TW_EUNSUPPORTED;
+    if (c_dtype == TW_F16) c_dtype = TW_BF16;
+    if (res_dtype == TW_F16) res_dtype = TW_BF16;
+  } else if (flags & F_CLAMP16) {
+    return TW_EINVAL;
+  }
   if (M > 4 || K <= 0 || (K % 8) || (ldx % 8) || (ldw % 8)) return TW_EINVAL;
   if (((uintptr_t)x & 15) || ((uintptr_t)W & 15)) return TW_EINVAL;
   if (ln_w && (!ln_b || (K % 256) || (((uintptr_t)ln_w | (uintptr_t)ln_b) & 15))) return TW_EINVAL;
@@ -1107,7 +1143,7 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
   const size_t lds = (size_t)(M == 1 ? 1 : M == 2 ? 2 : 4) * K * 2;
 #define TW_GEMV(MR_, CPW_, PRE_) \
-  hipLaunchKernelGGL((gemv_kernel<MR_, CPW_, PRE_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
+  hipLaunchKernelGGL((gemv_kernel<H, MR_, CPW_, PRE_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
   if (cpw == 8) {
     if (M == 1) TW_GEMV(1, 8, 3);
     else if (M == 2) TW_GEMV(2, 8, 3);
@@ -1124,4 +1160,42 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
 #undef TW_GEMV
   TW_CHECK_LAUNCH();
   return TW_OK;
+}
+
+}  // namespace
+
+extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
+                            void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
+                            int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
+                            const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
+                            void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
+  return gemm_run<false>(A, lda, a_trans, B, ldb, b_trans, C, ldc, c_dtype, M, N, K, batch, sA, sB, sC, alpha, bias,
+                         res, ldr, sR, res_dtype, res_mod, aux, ldaux, sAux, flags, stream);
+}
+
+extern "C" int tw_gemm_f16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
+                           void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
+                           int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
+                           const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
+                           void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
+  return gemm_run<true>(A, lda, a_trans, B, ldb, b_trans, C, ldc, c_dtype, M, N, K, batch, sA, sB, sC, alpha, bias,
+                        res, ldr, sR, res_dtype, res_mod, aux, ldaux, sAux, flags, stream);
+}
+
+extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
+                            int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
+                            const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
+                            void* kv_cache, int64_t kv_sb, int64_t kv_ld, int kv_col0, const int* t_dev,
+                            hipStream_t stream) {
+  return gemv_run<false>(x, ldx, ln_w, ln_b, eps, W, ldw, C, ldc, c_dtype, M, N, K, bias, res, ldr, res_dtype, aux,
+                         ldaux, flags, kv_cache, kv_sb, kv_ld, kv_col0, t_dev, stream);
+}
+
+extern "C" int tw_gemv_f16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
+                           int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
+                           const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
+                           void* kv_cache, int64_t kv_sb, int64_t kv_ld, int kv_col0, const int* t_dev,
+                           hipStream_t stream) {
+  return gemv_run<true>(x, ldx, ln_w, ln_b, eps, W, ldw, C, ldc, c_dtype, M, N, K, bias, res, ldr, res_dtype, aux,
+                        ldaux, flags, kv_cache, kv_sb, kv_ld, kv_col0, t_dev, stream);
 }

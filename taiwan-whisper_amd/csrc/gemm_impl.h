@@ -21,7 +21,16 @@ enum {
   F_ACCUM = 16,    // v += C_old
   F_AUX_OUT = 32,  // store pre-activation to aux (with F_GELU)
   F_DGELU = 64,    // v = bf16(v * gelu'(aux[m][n]))  (gelu backward, aux = pre-activation)
+  F_CLAMP16 = 128, // after the residual add: clamp to +-(fp16 max - 1000) (HF fp16 encoder layer, fp16 GEMMs only)
 };
+
+// Inside the kernels a 16-bit C / residual / aux (c_dtype, res_dtype == TW_BF16) holds the operand type of
+// the instantiation (template flag H: bf16 words, or fp16 words for the H = true instantiations); the host
+// entry points map TW_F16 to that code for the fp16 GEMMs.
+template <bool H>
+__device__ __forceinline__ float ld16_as_f32(const void* p, int dtype, int64_t i) {
+  return dtype == TW_BF16 ? e2f<H>(((const bf16*)p)[i]) : ((const float*)p)[i];
+}
 
 struct GemmP {
   const bf16* A; const bf16* B; void* C;
@@ -127,7 +136,7 @@ __device__ __forceinline__ void tile_coords(int tid, const GemmP& p, int& mt, in
 
 // Generic epilogue (any flag combination, ragged edges): lane holds C[m][n..n+3] of each 16x16
 // fragment (swapped-operand MFMA layout).
-template <int BM, int BN, int WM, int WN>
+template <bool H, int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                          int n0, int wm, int wn, int lane, int bz) {
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -146,7 +155,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
       if (flags & F_BIAS) {
         const bf16x4 t = *(const bf16x4*)(p.bias + n0 + wn * (BN / WN) + ni * 16 + 4 * g);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[ni][r] = bf2f(t[r]);
+        for (int r = 0; r < 4; ++r) bv[ni][r] = e2f<H>(t[r]);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
@@ -164,7 +173,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
           if (flags & F_DGELU) {
             const bf16x4 t = *(const bf16x4*)(p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ex[ni][r] = bf2f(t[r]);
+            for (int r = 0; r < 4; ++r) ex[ni][r] = e2f<H>(t[r]);
           } else {
             const bool res = flags & F_RES;
             const void* src = res ? p.res : (const void*)C;
@@ -173,7 +182,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
             if (dt == TW_BF16) {
               const bf16x4 t = *(const bf16x4*)((const bf16*)src + o);
 #pragma unroll
-              for (int r = 0; r < 4; ++r) ex[ni][r] = bf2f(t[r]);
+              for (int r = 0; r < 4; ++r) ex[ni][r] = e2f<H>(t[r]);
             } else {
               const f32x4 t = *(const f32x4*)((const float*)src + o);
 #pragma unroll
@@ -189,22 +198,26 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v[r] = p.alpha * acc[mi][ni][r] + bv[ni][r];
-          if (flags & F_ROUND) v[r] = rbf(v[r]);
-          if (flags & F_DGELU) v[r] = rbf(v[r] * gelu_erf_grad(ex[ni][r]));
+          if (flags & F_ROUND) v[r] = rnd<H>(v[r]);
+          if (flags & F_DGELU) v[r] = rnd<H>(v[r] * gelu_erf_grad(ex[ni][r]));
         }
         if (flags & F_GELU) {
           if (flags & F_AUX_OUT)
             *(bf16x4*)(p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n) =
-                bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_erf(v[r]));
+          for (int r = 0; r < 4; ++r) v[r] = rnd<H>(gelu_erf(v[r]));
         }
         if (flags & (F_RES | F_ACCUM)) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += ex[ni][r];
         }
+        if (flags & F_CLAMP16) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = clamp_f16_stream(rnd<H>(v[r]));
+        }
         const int64_t co = bz * p.sC + (int64_t)m * p.ldc + n;
-        if (p.c_dtype == TW_BF16) *(bf16x4*)((bf16*)C + co) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        if (p.c_dtype == TW_BF16) *(bf16x4*)((bf16*)C + co) = bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
         else *(f32x4*)((float*)C + co) = f32x4{v[0], v[1], v[2], v[3]};
       }
     }
@@ -224,39 +237,43 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
       const bool full = (n + 3 < p.N);
       const int nv = full ? 4 : (p.N - n);
       if (flags & F_BIAS) {
-        for (int r = 0; r < nv; ++r) v[r] += bf2f(p.bias[n + r]);
+        for (int r = 0; r < nv; ++r) v[r] += e2f<H>(p.bias[n + r]);
       }
       if (flags & F_ROUND) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = rbf(v[r]);
+        for (int r = 0; r < 4; ++r) v[r] = rnd<H>(v[r]);
       }
       if (flags & F_DGELU) {
         const bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
-        for (int r = 0; r < nv; ++r) v[r] = rbf(v[r] * gelu_erf_grad(bf2f(ax[r])));
+        for (int r = 0; r < nv; ++r) v[r] = rnd<H>(v[r] * gelu_erf_grad(e2f<H>(ax[r])));
       }
       if (flags & F_GELU) {
         if (flags & F_AUX_OUT) {
           bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
-          for (int r = 0; r < nv; ++r) ax[r] = f2bf(v[r]);
+          for (int r = 0; r < nv; ++r) ax[r] = f2e<H>(v[r]);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_erf(v[r]));
+        for (int r = 0; r < 4; ++r) v[r] = rnd<H>(gelu_erf(v[r]));
       }
       if (flags & F_RES) {
         const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
         const int64_t ro = bz * p.sR + (int64_t)mr * p.ldr + n;
-        for (int r = 0; r < nv; ++r) v[r] += ld_as_f32(p.res, p.res_dtype, ro + r);
+        for (int r = 0; r < nv; ++r) v[r] += ld16_as_f32<H>(p.res, p.res_dtype, ro + r);
       }
       const int64_t co = bz * p.sC + (int64_t)m * p.ldc + n;
       if (flags & F_ACCUM) {
-        for (int r = 0; r < nv; ++r) v[r] += ld_as_f32(C, p.c_dtype, co + r);
+        for (int r = 0; r < nv; ++r) v[r] += ld16_as_f32<H>(C, p.c_dtype, co + r);
+      }
+      if (flags & F_CLAMP16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = clamp_f16_stream(rnd<H>(v[r]));
       }
       if (p.c_dtype == TW_BF16) {
         bf16* cp = (bf16*)C + co;
         if (full && ((co & 3) == 0)) {
-          *(bf16x4*)cp = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          *(bf16x4*)cp = bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
         } else {
-          for (int r = 0; r < nv; ++r) cp[r] = f2bf(v[r]);
+          for (int r = 0; r < nv; ++r) cp[r] = f2e<H>(v[r]);
         }
       } else {
         float* cp = (float*)C + co;
@@ -284,30 +301,41 @@ enum { EPI_GENERIC = 0, EPI_STORE_BF16, EPI_STORE_F32, EPI_GELU, EPI_GELU_AUX, E
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+template <bool H>
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  return __builtin_bit_cast(uint32_t, bf16x2{f2bf(a), f2bf(b)});
+  return __builtin_bit_cast(uint32_t, bf16x2{f2e<H>(a), f2e<H>(b)});
 }
-__device__ __forceinline__ float lo_bf(uint32_t u) { return __builtin_bit_cast(float, u << 16); }
-__device__ __forceinline__ float hi_bf(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+template <bool H>
+__device__ __forceinline__ float lo_e(uint32_t u) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+  else return __builtin_bit_cast(float, u << 16);
+}
+template <bool H>
+__device__ __forceinline__ float hi_e(uint32_t u) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+  else return __builtin_bit_cast(float, u & 0xffff0000u);
+}
 
 // fragments X (ni) and Y (ni+1), 4 floats each -> this lane's 16 B of the pair (swapped layout)
+template <bool H>
 __device__ __forceinline__ u32x4 pair_to_u4(const float (&x)[4], const float (&y)[4]) {
-  const uint32_t x0 = pack2(x[0], x[1]), x1 = pack2(x[2], x[3]);
-  const uint32_t y0 = pack2(y[0], y[1]), y1 = pack2(y[2], y[3]);
+  const uint32_t x0 = pack2<H>(x[0], x[1]), x1 = pack2<H>(x[2], x[3]);
+  const uint32_t y0 = pack2<H>(y[0], y[1]), y1 = pack2<H>(y[2], y[3]);
   const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
   return u32x4{s0[0], s1[0], s0[1], s1[1]};
 }
 // inverse: this lane's 16 B of the pair (swapped layout) -> fragments X, Y as floats
+template <bool H>
 __device__ __forceinline__ void u4_to_pair(u32x4 r, float (&x)[4], float (&y)[4]) {
   const auto s0 = __builtin_amdgcn_permlane16_swap(r[0], r[2], false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(r[1], r[3], false, false);
-  x[0] = lo_bf(s0[0]); x[1] = hi_bf(s0[0]); x[2] = lo_bf(s1[0]); x[3] = hi_bf(s1[0]);
-  y[0] = lo_bf(s0[1]); y[1] = hi_bf(s0[1]); y[2] = lo_bf(s1[1]); y[3] = hi_bf(s1[1]);
+  x[0] = lo_e<H>(s0[0]); x[1] = hi_e<H>(s0[0]); x[2] = lo_e<H>(s1[0]); x[3] = hi_e<H>(s1[0]);
+  y[0] = lo_e<H>(s0[1]); y[1] = hi_e<H>(s0[1]); y[2] = lo_e<H>(s1[1]); y[3] = hi_e<H>(s1[1]);
 }
 
-template <int BM, int BN, int WM, int WN, int KIND>
+template <bool H, int BM, int BN, int WM, int WN, int KIND>
 __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                               int n0, int wm, int wn, int lane, int bz) {
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -315,14 +343,14 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
   const int g = lane >> 4, li = lane & 15;
   const int cw = n0 + wn * (BN / WN);                 // wave's first column
   const int sw = (g & 1) * 16 + (g >> 1) * 8;        // this lane's column in a swapped pair
-  const bool rnd = p.flags & F_ROUND;
+  const bool rd = p.flags & F_ROUND;
   float bv[FN][4];
 #pragma unroll
   for (int ni = 0; ni < FN; ++ni) {
     if (p.flags & F_BIAS) {
       const bf16x4 t = *(const bf16x4*)(p.bias + cw + ni * 16 + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[ni][r] = bf2f(t[r]);
+      for (int r = 0; r < 4; ++r) bv[ni][r] = e2f<H>(t[r]);
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
@@ -355,7 +383,7 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
         for (int r = 0; r < 4; ++r) v[h][r] = p.alpha * acc[mi][2 * np + h][r] + bv[2 * np + h][r];
       if constexpr (KIND == EPI_STORE_BF16) {
         bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        const u32x4 o = pair_to_u4(v[0], v[1]);
+        const u32x4 o = pair_to_u4<H>(v[0], v[1]);
         // (1 << 21): diagnostic, compute but do not store (timing only)
         if (!(p.flags & (1 << 21)) || o[0] == 0x7fc17fc1u) *(u32x4*)(crow + np * 32 + sw) = o;
       } else if constexpr (KIND == EPI_STORE_F32) {
@@ -364,17 +392,17 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
         for (int h = 0; h < 2; ++h) {
           f32x4 o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = rnd ? rbf(v[h][r]) : v[h][r];
+          for (int r = 0; r < 4; ++r) o[r] = rd ? rnd<H>(v[h][r]) : v[h][r];
           *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
         }
       } else if constexpr (KIND == EPI_GELU || KIND == EPI_GELU_AUX) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[h][r] = rbf(v[h][r]);     // autocast: Linear output is bf16
+          for (int r = 0; r < 4; ++r) v[h][r] = rnd<H>(v[h][r]);     // autocast: Linear output is bf16
         if constexpr (KIND == EPI_GELU_AUX) {
           bf16* arow = p.aux + bz * p.sAux + m * p.ldaux + cw;
-          *(u32x4*)(arow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+          *(u32x4*)(arow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -385,24 +413,31 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
             v[h][r + 1] = y.y;
           }
         bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
       } else if constexpr (KIND == EPI_RES_BF16) {
         float x[4], y[4];
-        u4_to_pair(rb[np], x, y);
+        u4_to_pair<H>(rb[np], x, y);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          v[0][r] = (rnd ? rbf(v[0][r]) : v[0][r]) + x[r];
-          v[1][r] = (rnd ? rbf(v[1][r]) : v[1][r]) + y[r];
+          v[0][r] = (rd ? rnd<H>(v[0][r]) : v[0][r]) + x[r];
+          v[1][r] = (rd ? rnd<H>(v[1][r]) : v[1][r]) + y[r];
+        }
+        if (p.flags & F_CLAMP16) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[0][r] = clamp_f16_stream(rnd<H>(v[0][r]));
+            v[1][r] = clamp_f16_stream(rnd<H>(v[1][r]));
+          }
         }
         bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4(v[0], v[1]);
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
       } else {   // EPI_RES_F32
         float* crow = (float*)p.C + bz * p.sC + m * p.ldc + cw;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           f32x4 o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (rnd ? rbf(v[h][r]) : v[h][r]) + rf[2 * np + h][r];
+          for (int r = 0; r < 4; ++r) o[r] = (rd ? rnd<H>(v[h][r]) : v[h][r]) + rf[2 * np + h][r];
           *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
         }
       }
@@ -410,18 +445,18 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <bool H, int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void epilogue(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                          int n0, int wm, int wn, int lane, int bz) {
   const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
   const int k = full ? p.epi : EPI_GENERIC;
-  if (k == EPI_STORE_BF16) epilogue_fast<BM, BN, WM, WN, EPI_STORE_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_STORE_F32) epilogue_fast<BM, BN, WM, WN, EPI_STORE_F32>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_GELU) epilogue_fast<BM, BN, WM, WN, EPI_GELU>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_GELU_AUX) epilogue_fast<BM, BN, WM, WN, EPI_GELU_AUX>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_RES_BF16) epilogue_fast<BM, BN, WM, WN, EPI_RES_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_RES_F32) epilogue_fast<BM, BN, WM, WN, EPI_RES_F32>(p, acc, m0, n0, wm, wn, lane, bz);
-  else epilogue_generic<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
+  if (k == EPI_STORE_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_STORE_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_F32>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_GELU) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_GELU_AUX) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU_AUX>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_RES_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_RES_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_RES_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_RES_F32>(p, acc, m0, n0, wm, wn, lane, bz);
+  else epilogue_generic<H, BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
 }
 
 __device__ __forceinline__ bool pp_tile(const GemmP& p, int i, int& m0, int& n0, int& bz) {

@@ -178,6 +178,9 @@ extern "C" int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, 
   if (logits_dtype == TW_BF16)
     hipLaunchKernelGGL(klce_kernel<bf16>, dim3(rows), dim3(NT), 0, stream, (const bf16*)s_logits, (const bf16*)t_logits,
                        ld, labels, V, T, ce_w, kl_w, n_valid, grad_scale, row_out, (bf16*)dlogits);
+  else if (logits_dtype == TW_F16)      // the fp16 model's eval CE (HF upcasts fp16 logits to fp32)
+    hipLaunchKernelGGL(klce_kernel<f16>, dim3(rows), dim3(NT), 0, stream, (const f16*)s_logits, (const f16*)t_logits,
+                       ld, labels, V, T, ce_w, kl_w, n_valid, grad_scale, row_out, (f16*)dlogits);
   else if (logits_dtype == TW_F32)
     hipLaunchKernelGGL(klce_kernel<float>, dim3(rows), dim3(NT), 0, stream, (const float*)s_logits,
                        (const float*)t_logits, ld, labels, V, T, ce_w, kl_w, n_valid, grad_scale, row_out,

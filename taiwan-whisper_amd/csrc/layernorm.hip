@@ -40,9 +40,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
         if (x_dtype == TW_F32) {
           f32x4 t = *(const f32x4*)((const float*)x + base + e);
           v[j][0] = t[0]; v[j][1] = t[1]; v[j][2] = t[2]; v[j][3] = t[3];
-        } else {
+        } else if (x_dtype == TW_BF16) {
           bf16x4 t = *(const bf16x4*)((const bf16*)x + base + e);
           v[j][0] = bf2f(t[0]); v[j][1] = bf2f(t[1]); v[j][2] = bf2f(t[2]); v[j][3] = bf2f(t[3]);
+        } else {
+          f16x4 t = *(const f16x4*)((const f16*)x + base + e);
+          v[j][0] = (float)t[0]; v[j][1] = (float)t[1]; v[j][2] = (float)t[2]; v[j][3] = (float)t[3];
         }
       } else {
         v[j][0] = ld_as_f32(x, x_dtype, base + e);
@@ -73,6 +76,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
       if (y_dtype == TW_BF16) {
         if (VEC == 4) *(bf16x4*)((bf16*)y + base + e) = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
         else ((bf16*)y)[base + e] = f2bf(o[0]);
+      } else if (y_dtype == TW_F16) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) ((f16*)y)[base + e + q] = (_Float16)o[q];
       } else {
         if (VEC == 4) *(f32x4*)((float*)y + base + e) = f32x4{o[0], o[1], o[2], o[3]};
         else ((float*)y)[base + e] = o[0];
@@ -86,7 +92,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 // reduced over the 32 lanes of the half (same two-pass mean / variance as ln_fwd_kernel).
 // ADD: x_out = bf16(x + r) first (the bf16 stream's residual update, the same fp32 add + one round as the
 // GEMM's residual epilogue), then the LayerNorm of x_out.
-template <int NCH, bool ADD = false>
+// H: the rows hold fp16 words (the fp16 stream of a torch_dtype=float16 model), else bf16
+template <int NCH, bool ADD = false, bool H = false>
 __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ b, bf16* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -105,11 +112,11 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
     if constexpr (ADD) {
       const bf16x8 u = ok ? *(const bf16x8*)(r + base + e) : bf16x8{};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) t[q] = f2bf(bf2f(t[q]) + bf2f(u[q]));
+      for (int q = 0; q < 8; ++q) t[q] = f2e<H>(e2f<H>(t[q]) + e2f<H>(u[q]));
       if (ok) *(bf16x8*)(x_out + base + e) = t;
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) { v[c][q] = bf2f(t[q]); s += v[c][q]; }
+    for (int q = 0; q < 8; ++q) { v[c][q] = e2f<H>(t[q]); s += v[c][q]; }
   }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -135,8 +142,8 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      o[q] = f2bf((v[c][q] - mean) * rstd * w0[q] + b0[q]);
-      o[q + 4] = f2bf((v[c][q + 4] - mean) * rstd * w1[q] + b1[q]);
+      o[q] = f2e<H>((v[c][q] - mean) * rstd * w0[q] + b0[q]);
+      o[q + 4] = f2e<H>((v[c][q + 4] - mean) * rstd * w1[q] + b1[q]);
     }
     *(bf16x8*)(y + base + e) = o;
   }
@@ -250,7 +257,23 @@ extern "C" int tw_layernorm_fwd(const void* x, int x_dtype, const float* w, cons
   if (D % 64 || D > 1280) return TW_EUNSUPPORTED;
   dim3 grid((rows + WPB - 1) / WPB), block(64 * WPB);
   const bool a16 = (((uintptr_t)x | (uintptr_t)y | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
-  if (x_dtype == TW_BF16 && y_dtype == TW_BF16 && D % 256 == 0 && a16) {
+  if (x_dtype == TW_F16 && y_dtype == TW_F16 && D % 256 == 0 && a16) {
+    const dim3 g2((rows + 2 * WPB - 1) / (2 * WPB));
+    const bf16* xb = (const bf16*)x;
+    bf16* yb = (bf16*)y;
+    switch (D / 256) {
+      case 1: hipLaunchKernelGGL((ln_fwd_bf16_kernel<1, false, true>), g2, block, 0, stream, xb, w, b, yb, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      case 2: hipLaunchKernelGGL((ln_fwd_bf16_kernel<2, false, true>), g2, block, 0, stream, xb, w, b, yb, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      case 3: hipLaunchKernelGGL((ln_fwd_bf16_kernel<3, false, true>), g2, block, 0, stream, xb, w, b, yb, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      case 4: hipLaunchKernelGGL((ln_fwd_bf16_kernel<4, false, true>), g2, block, 0, stream, xb, w, b, yb, mean_out,
+                                 rstd_out, rows, D, eps); break;
+      default: hipLaunchKernelGGL((ln_fwd_bf16_kernel<5, false, true>), g2, block, 0, stream, xb, w, b, yb, mean_out,
+                                  rstd_out, rows, D, eps); break;
+    }
+  } else if (x_dtype == TW_BF16 && y_dtype == TW_BF16 && D % 256 == 0 && a16) {
     const dim3 g2((rows + 2 * WPB - 1) / (2 * WPB));
     switch (D / 256) {
       case 1: hipLaunchKernelGGL(ln_fwd_bf16_kernel<1>, g2, block, 0, stream, (const bf16*)x, w, b, (bf16*)y, mean_out,

@@ -19,8 +19,7 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const void* __
     const float a = ld_as_f32(tok, tok_dtype, id * D + e);
     const float b = ld_as_f32(pos, pos_dtype, (int64_t)t * D + e);
     const float s = a + b;
-    if (out_dtype == TW_BF16) ((bf16*)out)[(int64_t)row * D + e] = f2bf(s);
-    else ((float*)out)[(int64_t)row * D + e] = s;
+    st_from_f32(out, out_dtype, (int64_t)row * D + e, s);
   }
 }
 
@@ -198,8 +197,10 @@ __global__ void count_valid_kernel(const int64_t* __restrict__ labels, int64_t n
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
 
-// mel [B][80][3000] f32 -> time-major bf16 conv1 input [B][3002][80] with zero rows 0 and 3001
-__global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, bf16* __restrict__ xt, int B, int nmel,
+// mel [B][80][3000] f32 -> time-major 16-bit conv1 input [B][3002][80] with zero rows 0 and 3001 (E = bf16:
+// the autocast cast of the Conv1d input; E = f16: run_eval.py:589 input_features.to(float16))
+template <typename E>
+__global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, E* __restrict__ xt, int B, int nmel,
                                          int T) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = (int64_t)B * (T + 2) * nmel;
@@ -209,7 +210,7 @@ __global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, bf16* __
   const int b = r / (T + 2), tt = r % (T + 2);
   float v = 0.f;
   if (tt >= 1 && tt <= T) v = mel[((int64_t)b * nmel + c) * T + (tt - 1)];
-  xt[i] = f2bf(v);
+  from_f32(xt[i], v);
 }
 
 // out = bf16( round?(g) * gelu'(pre) )  — GELU backward on an autocast bf16 activation
@@ -368,8 +369,17 @@ extern "C" int tw_count_valid(const int64_t* labels, int64_t n, int* out, hipStr
 extern "C" int tw_mel_to_conv_input(const float* mel, void* xt, int B, int nmel, int T, hipStream_t stream) {
   const int64_t n = (int64_t)B * (T + 2) * nmel;
   if (n <= 0) return TW_OK;
-  hipLaunchKernelGGL(mel_to_conv_input_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, mel, (bf16*)xt, B, nmel,
-                     T);
+  hipLaunchKernelGGL(mel_to_conv_input_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, stream, mel, (bf16*)xt, B,
+                     nmel, T);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_mel_to_conv_input_f16(const float* mel, void* xt, int B, int nmel, int T, hipStream_t stream) {
+  const int64_t n = (int64_t)B * (T + 2) * nmel;
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(mel_to_conv_input_kernel<f16>, dim3((n + 255) / 256), dim3(256), 0, stream, mel, (f16*)xt, B,
+                     nmel, T);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

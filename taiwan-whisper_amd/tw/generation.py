@@ -72,8 +72,8 @@ class DecodeSession:
         # batch <= 4 on the bf16 path: every Linear is one tw_gemv_bf16 launch, with the LayerNorm in front
         # of it fused when the residual stream is bf16 (bit-identical A); larger batches use the skinny
         # GEMM with a separate LayerNorm
-        self.gemv = B <= 4 and model.compute == "bf16" and d % 256 == 0
-        self.gemv_ln = self.gemv and model.stream_dtype == torch.bfloat16
+        self.gemv = B <= 4 and model.compute in ("bf16", "fp16") and d % 256 == 0
+        self.gemv_ln = self.gemv and model.stream_dtype == act
 
     def set_encoder(self, enc16):
         """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe)."""

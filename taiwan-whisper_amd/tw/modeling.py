@@ -123,7 +123,7 @@ def to_hf(name, v: torch.Tensor, cfg: WhisperConfig):
 class ParamStore:
     """Flat device buffers with named engine-layout views."""
 
-    def __init__(self, segs, device, master: bool, order=None):
+    def __init__(self, segs, device, master: bool, order=None, half=torch.bfloat16):
         self.segs = dict(segs)
         names = [n for n, _ in segs] if order is None else list(order)
         self.order = names
@@ -135,7 +135,9 @@ class ParamStore:
         self.total = off
         self.device = device
         self.p32 = torch.zeros(off, dtype=torch.float32, device=device) if master else None
-        self.p16 = torch.zeros(off, dtype=torch.bfloat16, device=device)
+        # the 16-bit copy the GEMMs read: the bf16 mirror (autocast's weight cast), or the fp16 weights of a
+        # torch_dtype=float16 model
+        self.p16 = torch.zeros(off, dtype=half, device=device)
 
     def numel(self, n):
         return int(np.prod(self.segs[n]))
@@ -203,10 +205,13 @@ class WhisperForConditionalGeneration:
     main_input_name = "input_features"
 
     def __init__(self, config: WhisperConfig, dtype=torch.float32, device="cuda", compute: str = "bf16"):
-        """dtype: parameter storage (fp32 master + bf16 mirror, or bf16 only).  compute: "bf16" = CUDA bf16
-        autocast's rounding points (mixed_precision="bf16", every reference launcher); "fp32" = plain fp32
+        """dtype: parameter storage (fp32 master + bf16 mirror, bf16 only, or fp16 only).  compute: "bf16" = CUDA
+        bf16 autocast's rounding points (mixed_precision="bf16", every reference launcher); "fp32" = plain fp32
         arithmetic end to end (mixed_precision="no", the reference's default --dtype float32; needs the
-        fp32 master)."""
+        fp32 master); "fp16" = a torch_dtype=float16 model without autocast (run_eval.py:99,500-509 default
+        --dtype float16, run_pseudo_labelling.py:461-463): fp16 weights, fp16 Linear / attention outputs and
+        residual stream, LayerNorm statistics in fp32 with fp16 output, fp16 logits.  An fp16 model is
+        inference-only (the reference trains in bf16 or fp32)."""
         if isinstance(config, dict):
             config = WhisperConfig(**config)
         self.config = config
@@ -215,7 +220,10 @@ class WhisperForConditionalGeneration:
         self.device = torch.device(device)
         self.Vp = padded_vocab(config.vocab_size)
         self.segs = engine_segments(config)
-        self.store = ParamStore(self.segs, self.device, master=(dtype == torch.float32))
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            raise ValueError(f"unsupported parameter dtype {dtype}")
+        self.store = ParamStore(self.segs, self.device, master=(dtype == torch.float32),
+                                half=torch.float16 if dtype == torch.float16 else torch.bfloat16)
         self._ln32 = {}          # fp32 LayerNorm params for bf16 models
         self.trainable = set()   # HF names with requires_grad
         self.grad = None         # flat fp32 grads over the trainable prefix (see pack_for_training)
@@ -226,20 +234,23 @@ class WhisperForConditionalGeneration:
         self.model.encoder = _Group(self, "model.encoder")
         self.model.decoder = _Group(self, "model.decoder")
         self.proj_out = _Group(self, "model.decoder.embed_tokens")
-        self.set_compute(compute)
+        self.set_compute("fp16" if dtype == torch.float16 else compute)
 
     def set_compute(self, compute: str):
-        if compute not in ("bf16", "fp32"):
-            raise ValueError(f"compute must be 'bf16' or 'fp32', got {compute!r}")
+        if compute not in ("bf16", "fp32", "fp16"):
+            raise ValueError(f"compute must be 'bf16', 'fp16' or 'fp32', got {compute!r}")
         if compute == "fp32" and self.dtype != torch.float32:
             raise ValueError("fp32 arithmetic needs fp32 parameters (torch_dtype=torch.float32)")
+        if (compute == "fp16") != (self.dtype == torch.float16):
+            raise ValueError("fp16 arithmetic is the torch_dtype=float16 model (fp16 parameters), and only that")
         self.compute = compute
         return self
 
     @property
     def act_dtype(self):
-        """dtype of every GEMM / attention operand and output: bf16 under autocast, fp32 on the fp32 path."""
-        return torch.float32 if self.compute == "fp32" else torch.bfloat16
+        """dtype of every GEMM / attention operand and output: bf16 under autocast, fp32 on the fp32 path, fp16 for
+        an fp16 model."""
+        return {"fp32": torch.float32, "fp16": torch.float16}.get(self.compute, torch.bfloat16)
 
     def act_grad(self, g: torch.Tensor) -> torch.Tensor:
         """gradient entering a GEMM: rounded to bf16 under autocast (the grad of a bf16 activation),
@@ -249,7 +260,7 @@ class WhisperForConditionalGeneration:
     # ------------------------------------------------------------------ state dict / IO
     @property
     def stream_dtype(self):
-        return torch.float32 if self.dtype == torch.float32 else torch.bfloat16
+        return self.dtype
 
     def named_parameters(self):
         for n in self.store.order:
@@ -289,7 +300,7 @@ class WhisperForConditionalGeneration:
             eng = to_engine(n, t, self.config, shp)
             if self.store.p32 is not None:
                 self.store.v32(n).copy_(eng.to(torch.float32))
-            self.store.v16(n).copy_(eng.to(torch.bfloat16))
+            self.store.v16(n).copy_(eng.to(self.store.p16.dtype))
         unexpected = [k for k in sd if k not in self.store.segs and k != "proj_out.weight"]
         if strict and (missing or unexpected):
             raise RuntimeError(f"load_state_dict: missing {missing[:5]} unexpected {unexpected[:5]}")
@@ -320,7 +331,8 @@ class WhisperForConditionalGeneration:
         if isinstance(cfg, dict):
             cfg = WhisperConfig(**cfg)
         sd = load_file(os.path.join(path, "model.safetensors"))
-        m = cls.from_state_dict(cfg, sd, dtype=torch_dtype or torch.float32, device=device, compute=compute)
+        dt = torch_dtype or torch.float32
+        m = cls.from_state_dict(cfg, sd, dtype=dt, device=device, compute="fp16" if dt == torch.float16 else compute)
         gp = os.path.join(path, "generation_config.json")
         if os.path.exists(gp):
             with open(gp) as f:
@@ -462,16 +474,18 @@ class WhisperForConditionalGeneration:
         F.add_layernorm_fwd(x, pend, xn, self.ln_param(name + ".weight"), self.ln_param(name + ".bias"), y, mean, rstd)
         return xn, y
 
-    def _res_out(self, h, w, b, x, tape, kind):
+    def _res_out(self, h, w, b, x, tape, kind, clamp=False):
         """The stream-updating Linear -> (stream, pending update): deferred to the next LayerNorm
-        (defer_residual), else applied by the GEMM's residual epilogue."""
+        (defer_residual), else applied by the GEMM's residual epilogue.  clamp: the fp16 encoder layer's
+        saturation after its MLP residual (HF modeling_whisper.py:409-411), fused into that epilogue."""
         M, N = h.shape[0], w.shape[0]
         if self.defer_residual(kind):
             r = torch.empty(M, N, dtype=self.act_dtype, device=self.device)
             self._lin(h, w, b, r)
             return x, r
         out = torch.empty(M, N, dtype=self.stream_dtype, device=self.device) if tape is not None else x
-        self._lin(h, w, b, out, res=x)
+        flags = F.GEMM_ROUND | (F.GEMM_CLAMP16 if clamp and self.compute == "fp16" else 0)
+        self._lin(h, w, b, out, res=x, flags=flags)
         return out, None
 
     def _attn_block(self, x, p, B, T, causal, tape=None, pend=None):
@@ -514,7 +528,7 @@ class WhisperForConditionalGeneration:
             tape.append(("cross", p, dict(sv=sv, y=y, q=q, kv=kv, o=o, lse=lse, B=B, T=T, Tk=Tk)))
         return out
 
-    def _mlp_block(self, x, p, tape=None, pend=None):
+    def _mlp_block(self, x, p, tape=None, pend=None, clamp=False):
         M = x.shape[0]
         sv = {} if tape is not None else None
         x, y = self._ln_in(x, pend, p + ".final_layer_norm", sv)
@@ -523,7 +537,7 @@ class WhisperForConditionalGeneration:
         pre = torch.empty(M, f, dtype=self.act_dtype, device=self.device) if tape is not None else None
         self._lin(y, self._w16(p + ".fc1.weight"), self._w16(p + ".fc1.bias"), h, aux=pre,
                   flags=F.GEMM_ROUND | F.GEMM_GELU | (F.GEMM_AUX_OUT if tape is not None else 0))
-        out = self._res_out(h, self._w16(p + ".fc2.weight"), self._w16(p + ".fc2.bias"), x, tape, "mlp")
+        out = self._res_out(h, self._w16(p + ".fc2.weight"), self._w16(p + ".fc2.bias"), x, tape, "mlp", clamp=clamp)
         if tape is not None:
             tape.append(("mlp", p, dict(sv=sv, y=y, h=h, pre=pre)))
         return out
@@ -571,7 +585,7 @@ class WhisperForConditionalGeneration:
         for i in range(cfg.encoder_layers):
             p = f"model.encoder.layers.{i}"
             x, pend = self._attn_block(x, p + ".self_attn", B, T, False, tape, pend)
-            x, pend = self._mlp_block(x, p, tape, pend)
+            x, pend = self._mlp_block(x, p, tape, pend, clamp=True)
         sv = {} if tape is not None else None
         _, enc = self._ln_in(x, pend, "model.encoder.layer_norm", sv)
         if tape is not None:

@@ -11,8 +11,10 @@ import torch
 from ._native import call, query
 from .profiling import KernelTimer
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 GEMM_BIAS, GEMM_ROUND, GEMM_GELU, GEMM_RES, GEMM_ACCUM, GEMM_AUX_OUT, GEMM_DGELU = 1, 2, 4, 8, 16, 32, 64
+GEMM_CLAMP16 = 128     # fp16 GEMMs: clamp after the residual add (HF fp16 encoder layer, modeling_whisper.py:409-411)
+HALF = (torch.bfloat16, torch.float16)
 GEMM_TILE128, GEMM_TILE256, GEMM_TILE256x128, GEMM_TILE256PP = 256, 512, 1024, 2048   # forced tiles (A/B benchmarking)
 GEMM_NOSPLIT = 16384   # no split-K for dW-shaped calls (A/B benchmarking)
 
@@ -22,6 +24,8 @@ def _dt(t: torch.Tensor) -> int:
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.float16:
+        return F16
     raise TypeError(f"tw: unsupported dtype {t.dtype}")
 
 
@@ -49,8 +53,9 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
          ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0, algo_N=None,
          batch_inner=1, sA_in=0, sB_in=0, sC_in=0):
     """C[b] = epi(alpha * A[b] @ B[b]^T); A [M][K] (a_trans: [K][M]); B [N][K] (b_trans: [K][N]).
-    bf16 operands -> tw_gemm_bf16 (autocast rounding points); fp32 operands -> tw_gemm_f32 (the fp32
-    path: every operand and epilogue tensor fp32, nothing rounded)."""
+    bf16 operands -> tw_gemm_bf16 (autocast rounding points); fp16 operands -> tw_gemm_f16 (the fp16 model:
+    K-major operands only, every 16-bit tensor fp16); fp32 operands -> tw_gemm_f32 (the fp32 path: every
+    operand and epilogue tensor fp32, nothing rounded)."""
     if M <= 0 or N <= 0:
         return C
     if A.dtype == torch.float32 or B.dtype == torch.float32:
@@ -59,20 +64,25 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
                         sA=sA, sB=sB, sC=sC, sR=sR, sAux=sAux, algo_N=algo_N, batch_inner=batch_inner, sA_in=sA_in,
                         sB_in=sB_in, sC_in=sC_in)
     assert batch_inner == 1, "tw.gemm: two-level batches are an fp32-path feature"
-    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "tw.gemm: A and B must be bf16 (or both fp32)"
+    h = A.dtype
+    assert h in HALF and B.dtype == h, "tw.gemm: A and B must be both bf16, both fp16 (or both fp32)"
+    if h == torch.float16:
+        assert not a_trans and not b_trans, "tw.gemm: fp16 products are forward-only (K-major A and B)"
+    assert C.dtype in (h, torch.float32), "tw.gemm: C is the operand dtype or fp32"
     _need(A, (batch - 1) * sA + ((K - 1) * lda + M if a_trans else (M - 1) * lda + K), "gemm A")
     _need(B, (batch - 1) * sB + ((K - 1) * ldb + N if b_trans else (N - 1) * ldb + K), "gemm B")
     _need(C, (batch - 1) * sC + (M - 1) * ldc + N, "gemm C")
     if bias is not None:
-        assert bias.dtype == torch.bfloat16
+        assert bias.dtype == h
         _need(bias, N, "gemm bias")
         flags |= GEMM_BIAS
     if res is not None:
+        assert res.dtype in (h, torch.float32)
         rows = res_mod if res_mod > 0 else M
         _need(res, (batch - 1) * sR + (rows - 1) * ldr + N, "gemm residual")
         flags |= GEMM_RES
     if aux is not None:
-        assert aux.dtype == torch.bfloat16
+        assert aux.dtype == h
         _need(aux, (batch - 1) * sAux + (M - 1) * ldaux + N, "gemm aux")
     fam = "gemm_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
     if KernelTimer.active is not None and query("tw_gemm_backend", M, N, K, int(a_trans), int(b_trans), _dt(C),
@@ -80,7 +90,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
         fam += "_lt"                 # timed apart: this call runs on hipBLASLt (include/tw_hip.h tw_gemm_backend)
     flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
     KernelTimer.wrap(fam, flops, lambda: call(
-        "tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
+        "tw_gemm_f16" if h == torch.float16 else "tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
         M, N, K, batch, sA, sB, sC, float(alpha), _ptr(bias), _ptr(res), ldr, sR,
         _dt(res) if res is not None else F32, res_mod, _ptr(aux), ldaux, sAux, flags, _stream()))
     return C
@@ -92,19 +102,20 @@ def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=No
     t_dev, t_max): columns >= col0 also go to cache row *t_dev (the fused KV append)."""
     M, K = x.shape
     N = W.shape[0]
-    assert x.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and M <= 4 and W.shape[1] == K
+    h = x.dtype
+    assert h in HALF and W.dtype == h and M <= 4 and W.shape[1] == K
     assert x.stride(1) == 1 and W.is_contiguous()
     _need(C, (M - 1) * C.stride(0) + N, "gemv C")
     if ln_w is not None:
         assert ln_w.dtype == torch.float32 and ln_b.dtype == torch.float32 and ln_w.numel() == K == ln_b.numel()
     if bias is not None:
-        assert bias.dtype == torch.bfloat16 and bias.numel() >= N
+        assert bias.dtype == h and bias.numel() >= N
         flags |= GEMM_BIAS
     if res is not None:
         _need(res, (M - 1) * res.stride(0) + N, "gemv residual")
         flags |= GEMM_RES
     if aux is not None:
-        assert aux.dtype == torch.bfloat16
+        assert aux.dtype == h
         _need(aux, (M - 1) * aux.stride(0) + N, "gemv aux")
     kc, ksb, kld, kcol, kt = None, 0, 0, 0, None
     if kv is not None:
@@ -112,7 +123,7 @@ def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=No
         assert kc.dtype == C.dtype and kt.dtype == torch.int32 and 0 <= kcol < N
         _need(kc, (M - 1) * ksb + (tmax - 1) * kld + (N - kcol), "gemv kv cache")
     KernelTimer.wrap("gemv", 2.0 * M * N * K, lambda: call(
-        "tw_gemv_bf16", x.data_ptr(), x.stride(0), _ptr(ln_w), _ptr(ln_b), float(eps), W.data_ptr(), K, C.data_ptr(),
+        "tw_gemv_f16" if h == torch.float16 else "tw_gemv_bf16", x.data_ptr(), x.stride(0), _ptr(ln_w), _ptr(ln_b), float(eps), W.data_ptr(), K, C.data_ptr(),
         C.stride(0), _dt(C), M, N, K, _ptr(bias), _ptr(res), res.stride(0) if res is not None else 0,
         _dt(res) if res is not None else F32, _ptr(aux), aux.stride(0) if aux is not None else 0, flags,
         _ptr(kc), ksb, kld, kcol, _ptr(kt), _stream()))
@@ -165,11 +176,11 @@ def attn_fwd(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale):
         return attn_fwd_f32(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Tq, Tk, causal, scale)
     hd = 64
     for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o")):
-        assert t.dtype == torch.bfloat16
+        assert t.dtype == q.dtype and t.dtype in HALF, nm
         _need(t, (B * T - 1) * ld + H * hd, f"attn {nm}")
     if lse is not None:
         _need(lse, B * H * Tq, "attn lse")
-    call("tw_attn_fwd", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, _ptr(lse),
+    call("tw_attn_fwd_f16" if q.dtype == torch.float16 else "tw_attn_fwd", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, _ptr(lse),
          B, H, Tq, Tk, hd, int(causal), float(scale), _stream())
     return o
 
@@ -196,7 +207,7 @@ def kl_ce(s_logits, t_logits, labels, V, n_valid, T=2.0, ce_w=0.8, kl_w=1.0, gra
           row_out=None, out3=None):
     rows, ld = s_logits.shape
     assert t_logits.shape == s_logits.shape and s_logits.dtype == t_logits.dtype
-    assert s_logits.dtype in (torch.bfloat16, torch.float32)
+    assert s_logits.dtype in (torch.bfloat16, torch.float16, torch.float32)   # fp16: eval CE of an fp16 model
     assert labels.dtype == torch.int64 and labels.numel() == rows and n_valid.dtype == torch.int32
     if row_out is None:
         row_out = torch.empty(rows * 2, dtype=torch.float32, device=s_logits.device)
@@ -236,8 +247,9 @@ def mel_to_conv_input(mel, xt):
     if xt.dtype == torch.float32:
         call("tw_mel_to_conv_input_f32", mel.data_ptr(), xt.data_ptr(), B, nmel, T, _stream())
         return xt
-    assert xt.dtype == torch.bfloat16
-    call("tw_mel_to_conv_input", mel.data_ptr(), xt.data_ptr(), B, nmel, T, _stream())
+    assert xt.dtype in HALF
+    call("tw_mel_to_conv_input_f16" if xt.dtype == torch.float16 else "tw_mel_to_conv_input", mel.data_ptr(),
+         xt.data_ptr(), B, nmel, T, _stream())
     return xt
 
 
@@ -358,7 +370,7 @@ def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_de
     With tk_dev the host cannot know Tk: tk_max bounds the rows checked for extent."""
     hd = 64
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
-        assert t.dtype == q.dtype and t.dtype in (torch.bfloat16, torch.float32), nm
+        assert t.dtype == q.dtype and t.dtype in (torch.bfloat16, torch.float16, torch.float32), nm
     rows = Tk if tk_dev is None else tk_max
     _need(q, (B - 1) * sqb + H * hd, "decode q")
     _need(k, (B - 1) * skb + (rows - 1) * ldk + H * hd, "decode k")
@@ -388,7 +400,7 @@ def token_bitmask(ids, V, device):
 
 def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids,
                   t_dev=None, begin_col=-1):
-    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and ids.dtype == torch.int64
     assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8
     _need(logits, (B - 1) * ld + V, "greedy logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "greedy ids")
@@ -403,7 +415,7 @@ def greedy_select(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos,
 
 def greedy_select_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids, col, next_ids, last_ts,
                      begin_col, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
-    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and ids.dtype == torch.int64
     assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8 and last_ts.dtype == torch.int32
     _need(logits, (B - 1) * ld + V, "greedy logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "greedy ids")
@@ -423,7 +435,7 @@ def select_sample(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos,
     + running log-prob of the chosen token (sum_logp: float32[B])."""
     assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
     _need(sum_logp, B, "select sum_logp")
-    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and ids.dtype == torch.int64
     assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8
     _need(logits, (B - 1) * ld + V, "select logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "select ids")
@@ -437,7 +449,7 @@ def select_sample_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids
                      ctl, sum_logp, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
     assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
     _need(sum_logp, B, "select sum_logp")
-    assert logits.dtype in (torch.bfloat16, torch.float32) and ids.dtype == torch.int64
+    assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and ids.dtype == torch.int64
     assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8 and last_ts.dtype == torch.int32
     _need(logits, (B - 1) * ld + V, "select logits")
     _need(ids, (B - 1) * ids.stride(0) + (ids.shape[1] if t_dev is not None else col + 1), "select ids")
@@ -450,7 +462,7 @@ def select_sample_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids
 
 def token_logprob(logits, ld, B, V, token, out):
     """out[b] = log_softmax(logits[b, :V])[token] (float32)."""
-    assert logits.dtype in (torch.bfloat16, torch.float32) and out.dtype == torch.float32
+    assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and out.dtype == torch.float32
     _need(logits, (B - 1) * ld + V, "token_logprob logits"); _need(out, B, "token_logprob out")
     call("tw_token_logprob", logits.data_ptr(), ld, _dt(logits), B, V, int(token), out.data_ptr(), _stream())
     return out
@@ -482,7 +494,7 @@ def embed_step(ids, tok, pos, out, t_dev, max_pos):
 
 
 def kv_append(src, ld_src, cache, ld_row, sb, B, n, t_dev, max_rows):
-    assert src.dtype == cache.dtype and src.dtype in (torch.bfloat16, torch.float32) and t_dev.dtype == torch.int32
+    assert src.dtype == cache.dtype and src.dtype in (torch.bfloat16, torch.float16, torch.float32) and t_dev.dtype == torch.int32
     _need(src, (B - 1) * ld_src + n, "kv_append src")
     _need(cache, (B - 1) * sb + (max_rows - 1) * ld_row + n, "kv_append cache")
     call("tw_kv_append", src.data_ptr(), ld_src, cache.data_ptr(), ld_row, sb, B, n, _dt(src), t_dev.data_ptr(),
@@ -491,7 +503,7 @@ def kv_append(src, ld_src, cache, ld_row, sb, B, n, t_dev, max_rows):
 
 def kv_head_major(src, ld, dst, B, Tk, H):
     """Row-interleaved cross K/V [B*Tk][ld] -> head-major K [B][H][Tk][64] then V (include/tw_hip.h)."""
-    assert src.dtype == dst.dtype and src.dtype in (torch.bfloat16, torch.float32)
+    assert src.dtype == dst.dtype and src.dtype in (torch.bfloat16, torch.float16, torch.float32)
     _need(src, (B * Tk - 1) * ld + 2 * 64 * H, "kv_head_major src")
     _need(dst, 2 * B * H * Tk * 64, "kv_head_major dst")
     call("tw_kv_head_major", src.data_ptr(), ld, dst.data_ptr(), B, Tk, H, _dt(src), _stream())

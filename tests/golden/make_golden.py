@@ -15,6 +15,7 @@ What produces each vector:
     (`training/create_student_model.py:99-226`, imported from /root/reference)
     and `mix_language_embeddings` (`utils/model_utils.py:4-14`)         -> student.npz
   * HF `generate(num_beams=1)` greedy with forced prompt                 -> greedy.npz
+  * the same forward / greedy / timestamp / long-form runs with torch_dtype=float16 -> fp16.npz
 
 Only small slices / checksums are stored (fixtures are data, no reference source).
 """
@@ -311,6 +312,71 @@ def gen_fallback(out):
     out["fb_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
 
 
+def gen_fp16(out):
+    """HF Whisper with torch_dtype=float16 (no autocast) on CPU -- the arithmetic of the reference's fp16 decode
+    call sites (run_eval.py:99 --dtype float16 default, :500-509 model.to(dtype), :589 input_features.to(dtype);
+    run_pseudo_labelling.py:461-463 via run-pseudo-labelling.sh:30): fp16 weights, fp16 Linear / conv / SDPA
+    outputs and residual stream, LayerNorm and GELU computed in fp32 with fp16 results, fp16 logits.
+      f16_enc_sub / f16_s_rows / f16_s_lse: forward of the micro_step batch (micro weights, seed 1)
+      f16_greedy_ids:   generate() greedy, the greedy.npz setup (lin_std 0.2 weights, 3 clips, max_length 64)
+      f16_ts_short_ids / f16_ts_long_ids: the greedy_ts.npz setup (timestamps, 65 s long-form)
+      f16_fb_cond_ids / f16_fb_avg_logprobs / f16_fb_ns_probs: the fallback.npz conditioned long-form run"""
+    cfg = CONFIGS["micro"]
+    # forward
+    m = hf_model(cfg, make_weights(cfg, 1), torch.float16).eval()
+    feats, dec, lab, _ = micro_batch()
+    with torch.no_grad():
+        o = m(input_features=torch.from_numpy(feats).half(), decoder_input_ids=torch.from_numpy(dec))
+    out["f16_enc_sub"] = o.encoder_last_hidden_state.float().numpy()[:, ::50, :]
+    lg = o.logits.float()
+    out["f16_s_lse"] = torch.logsumexp(lg, -1).numpy()
+    out["f16_s_argmax"] = lg.argmax(-1).numpy()
+    out["f16_s_rows"] = lg[:, ROWS, ::VSTRIDE].numpy()
+    # greedy
+    from transformers import GenerationConfig
+    m = hf_model(cfg, make_weights(cfg, 1, lin_std=0.2), torch.float16).eval()
+    gfe = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0),
+                                                 logmel.synthetic_clip(4, 25.0)])).half()
+    prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
+    m.generation_config = GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
+                                           pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
+                                           begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=64, num_beams=1,
+                                           do_sample=False, no_timestamps_token_id=SPECIAL["notimestamps"])
+    with torch.no_grad():
+        out["f16_greedy_ids"] = m.generate(gfe, decoder_input_ids=torch.tensor([prompt] * 3), max_length=64,
+                                           num_beams=1, do_sample=False).numpy()
+    # timestamps, long-form, conditioning + gates
+    m.generation_config = ts_generation_config()
+    tfe = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0)])).half()
+    lf = torch.from_numpy(longform_features()).half()
+    am = torch.ones(1, lf.shape[-1], dtype=torch.long)
+    kw = dict(return_timestamps=True, language="zh", task="transcribe")
+    rec = {"avg": [], "ns": []}
+    orig_need = type(m)._need_fallback
+
+    def spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size, temperature):
+        scores = seek_outputs[index]["scores"]
+        rec["avg"].append(float(self._retrieve_avg_logprobs(scores, seek_sequence, temperature)))
+        from transformers.generation.logits_process import WhisperNoSpeechDetection
+        for p_ in logits_processor or []:
+            if isinstance(p_, WhisperNoSpeechDetection):
+                rec["ns"].append(float(p_.no_speech_prob[index]))
+        return orig_need(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
+                         temperature)
+    with torch.no_grad():
+        out["f16_ts_short_ids"] = m.generate(tfe, max_new_tokens=48, **kw).numpy()
+        out["f16_ts_long_ids"] = m.generate(lf, attention_mask=am, **kw).numpy()
+        out["f16_fb_cond_ids"] = m.generate(lf, attention_mask=am, condition_on_prev_tokens=True, temperature=0.0,
+                                            **kw).numpy()
+        type(m)._need_fallback = spy
+        try:
+            m.generate(lf, attention_mask=am, temperature=(0.0,), logprob_threshold=-1e9, no_speech_threshold=1.0, **kw)
+        finally:
+            type(m)._need_fallback = orig_need
+    out["f16_fb_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
+    out["f16_fb_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
+
+
 # ------------------------------------------------------------------------------------------------
 # BASELINE-config parity fixtures (c1 / c2 / c3 dims).  The reference path is HF Whisper under
 # bf16 autocast (run_distillation.py:815-830 mixed_precision="bf16"; accelerate wraps every prepared
@@ -444,7 +510,7 @@ def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
     for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
-                     ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback),
+                     ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
                      ("cfg_c3", lambda o: gen_cfg("c3", o))):
         if only and name not in only:

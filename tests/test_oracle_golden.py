@@ -219,3 +219,58 @@ def test_longform_fallback_and_conditioning_match_hf():
     assert skip == [] and g["fb_skipall_ids"].shape[1] == 0
     np.testing.assert_allclose([t["avg_logprob"] for t in trace], g["fb_avg_logprobs"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose([t["no_speech_prob"] for t in trace], g["fb_ns_probs"], rtol=1e-3)
+
+
+# ---- fp16 (torch_dtype=float16, the reference's decode default: run_eval.py:99, run_pseudo_labelling.py:461-463)
+def _f16_ref(lin_std=0.02):
+    cfg = CONFIGS["micro"]
+    w = make_weights(cfg, 1, lin_std=lin_std)
+    return cfg, Ref(cfg, to_torch(w, torch.float16), amp=True, stream_bf16=True, half=torch.float16)
+
+
+def test_fp16_forward_matches_hf():
+    """The oracle's fp16 mode (fp16 rounding points, fp16 stream, encoder clamp) vs HF fp16 on CPU."""
+    g, h = load_golden("micro_step"), load_golden("fp16")
+    _, m = _f16_ref()
+    feats, dec = torch.from_numpy(g["feats"]), torch.from_numpy(g["dec"])
+    with torch.no_grad():
+        o = m.forward(feats, dec)
+    enc = o["enc"].numpy()[:, ::50]
+    # outputs are fp16 values: within 2 fp16 ulps of the row scale (HF's CPU fp16 GEMM / SDPA reduce in a
+    # different order than this fp32-accumulating restatement)
+    scale = np.abs(h["f16_enc_sub"]).max(-1, keepdims=True)
+    assert (np.abs(enc - h["f16_enc_sub"]) <= 2 * 2.0 ** -10 * scale).mean() >= 0.999
+    np.testing.assert_allclose(torch.logsumexp(o["logits"], -1).numpy(), h["f16_s_lse"], rtol=2e-3)
+    rows = o["logits"][:, [0, 3, 4, 57, 200, 446], ::97].numpy()
+    assert np.abs(rows - h["f16_s_rows"]).max() <= 4 * 2.0 ** -10 * np.abs(h["f16_s_rows"]).max()
+    assert (o["logits"].argmax(-1).numpy() == h["f16_s_argmax"]).mean() >= 0.99
+
+
+def test_fp16_greedy_timestamps_longform_match_hf():
+    h = load_golden("fp16")
+    cfg, m = _f16_ref(lin_std=0.2)
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as mg
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0),
+                                                   logmel.synthetic_clip(4, 25.0)]))
+    prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
+    with torch.no_grad():
+        ids = greedy_ref.greedy(m, feats, prompt, max_length=64 + 4, suppress_tokens=mg.SUPPRESS)
+    np.testing.assert_array_equal(ids.numpy()[:, 4:], h["f16_greedy_ids"])
+    tp = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"]]
+    with torch.no_grad():
+        ts = greedy_ref.greedy_ts(m, feats[:2], tp, max_length=len(tp) + 48, suppress_tokens=mg.SUPPRESS,
+                                  max_initial=50)
+    np.testing.assert_array_equal(ts[:, len(tp):].numpy(), h["f16_ts_short_ids"])
+    lf = torch.from_numpy(mg.longform_features())[0]
+    kw = dict(suppress_tokens=mg.SUPPRESS, max_initial=50)
+    with torch.no_grad():
+        assert greedy_ref.longform(m, lf, tp, **kw) == h["f16_ts_long_ids"][0].tolist()
+        assert greedy_ref.longform(m, lf, tp, condition_on_prev_tokens=True, **kw) == h["f16_fb_cond_ids"][0].tolist()
+        trace = []
+        greedy_ref.longform(m, lf, tp, logprob_threshold=-1e9, no_speech_threshold=1.0, trace=trace, **kw)
+    # the average of fp16 logits' log-softmax: within two fp16 ulps of the logit scale (|logit| < 4: 2^-8 each)
+    np.testing.assert_allclose([t["avg_logprob"] for t in trace], h["f16_fb_avg_logprobs"], rtol=0, atol=2.0 ** -7)
+    np.testing.assert_allclose([t["no_speech_prob"] for t in trace], h["f16_fb_ns_probs"], rtol=1e-2)
