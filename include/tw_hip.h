@@ -10,7 +10,7 @@
  *
  * Conventions
  *   - plain device pointers, int64 leading dimensions in ELEMENTS, row-major;
- *   - dtype codes: 0 = fp32, 1 = bf16;
+ *   - dtype codes: 0 = fp32, 1 = bf16, 2 = fp16;
  *   - every call is stream-ordered on `stream` (a hipStream_t), never synchronises,
  *     never allocates; workspaces are caller-provided;
  *   - return 0 on success, 1 = invalid argument/shape, 2 = unsupported, 3 = HIP launch error;
@@ -243,6 +243,33 @@ int tw_mel_to_conv_input_f32(const float* mel, float* xt, int B, int nmel, int T
 int tw_im2col3_f32(const float* src, int64_t src_rows, float* dst, int B, int T_out, int stride, int C,
                    tw_stream_t stream);
 int tw_gelu_bwd_f32(const float* g, const float* pre, float* out, int64_t n, tw_stream_t stream);
+
+/* ---- fp16 arithmetic path: a torch_dtype=float16 model without autocast, the arithmetic of the reference's fp16
+ * decode call sites (training/run_eval.py:99 `--dtype float16` default, :500-509 `model.to(dtype)`, :589
+ * `input_features.to(dtype)`; training/run_pseudo_labelling.py:461-463 under run-pseudo-labelling.sh:30):
+ * v_mfma_f32_16x16x32_f16 with fp32 accumulation, every 16-bit operand / output IEEE fp16 (RNE).
+ * tw_gemm_f16: tw_gemm_bf16 for fp16 operands, forward products only (a_trans = b_trans = 0; else 2);
+ *   A, B, bias, aux fp16; C and res fp16 (code 2) or fp32; epilogue order as tw_gemm_bf16 with the rounding
+ *   to fp16, plus TW_GEMM_CLAMP16: after the residual add, clamp to +-(65504 - 1000) (HF WhisperEncoderLayer,
+ *   modeling_whisper.py:409-411, the fp16 encoder stream).  Never routed to hipBLASLt.
+ * tw_gemv_f16: tw_gemv_bf16 for fp16 x / W / bias / C (LayerNorm fused as there, fp16 output of the LN).
+ * tw_attn_fwd_f16: tw_attn_fwd for fp16 Q/K/V/O (P rounded to fp16 for the PV product, fp32 row sums).
+ * tw_mel_to_conv_input_f16: log-mel [B][80][T] fp32 -> fp16 conv1 input [B][T+2][80] (the .to(float16) cast).
+ * The dtype-coded entries above (tw_layernorm_fwd, tw_embed_fwd / tw_embed_step, tw_decode_attn, the selection
+ * kernels, tw_token_logprob, tw_kv_append, tw_kv_head_major, tw_kl_ce) take code 2 for fp16 rows. */
+#define TW_GEMM_CLAMP16 128
+int tw_gemm_f16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans, void* C,
+                int64_t ldc, int c_dtype, int M, int N, int K, int batch, int64_t sA, int64_t sB, int64_t sC,
+                float alpha, const void* bias, const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
+                void* aux, int64_t ldaux, int64_t sAux, int flags, tw_stream_t stream);
+int tw_gemv_f16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
+                int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
+                const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
+                void* kv_cache, int64_t kv_sb, int64_t kv_ld, int kv_col0, const int* t_dev, tw_stream_t stream);
+int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv, void* O,
+                    int64_t ldo, float* lse, int B, int H, int Tq, int Tk, int head_dim, int causal, float scale,
+                    tw_stream_t stream);
+int tw_mel_to_conv_input_f16(const float* mel, void* xt, int B, int nmel, int T, tw_stream_t stream);
 
 /* ---- host code: FLAC decoding for the data feed (replaces soundfile / libsndfile's sf.read of the
  * reference corpus, dataset/cool_dataset.py:55).  `data` is the whole file in host memory.

@@ -164,6 +164,16 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x * (x >= 0.f ? 1.0f - h : h);
 }
 
+// GELU of the instantiation's operand type: bf16 -> the branch-free polynomial above (every bf16 result within
+// 1 ulp of torch's fp32 formula, tools/gelu_sweep.py); fp16 (10-bit mantissa, subnormals down to 6e-8) -> torch's
+// own formula x/2 (1 + erf(x/sqrt2)) with the device erff: the polynomial's 1.5e-7 absolute error is ~2 fp16
+// ulps of the small negative outputs, where the reference's fp32 formula is what it is
+template <bool H>
+__device__ __forceinline__ float gelu_of(float x) {
+  if constexpr (H) return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  else return gelu_erf(x);
+}
+
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752440f));
   const float pdf = 0.39894228040143267794f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);

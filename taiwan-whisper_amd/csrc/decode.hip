@@ -229,7 +229,7 @@ struct SelP {
   int64_t* next;              // [B] next-step input ids
   const int* t_dev;           // nullable: col = *t_dev + col, begin mask applied when col == begin_col
   int begin_col;
-  const uint32_t* ctl;        // nullable: [0] = bits of 1/T (0: greedy), [1], [2] = seed lo, hi
+  const uint32_t* ctl;        // nullable: per row b, ctl[3b] = bits of 1/T (0: greedy), ctl[3b+1], [3b+2] = seed lo, hi
   float* sum_logp;            // nullable: += log-prob of the chosen token while the row is live
   int vec;                    // rows 16-B aligned and padded to a multiple of 8 ids: 16-B loads
 };
@@ -279,9 +279,12 @@ __device__ __forceinline__ float gumbel(uint64_t seed, int b, int col, int v) {
   return -__logf(-__logf(u));
 }
 
-__device__ __forceinline__ void read_ctl(const uint32_t* ctl, float& inv_t, uint64_t& seed) {
-  inv_t = ctl ? __uint_as_float(ctl[0]) : 0.f;
-  seed = ctl ? ((uint64_t)ctl[2] << 32 | ctl[1]) : 0ull;
+// row b's sampling control: its own temperature and seed, so the rows of one batch can be independent fallback
+// attempts (each row's draw keyed by (its seed, column, id) only: a row decodes the same tokens whatever batch
+// it runs in)
+__device__ __forceinline__ void read_ctl(const uint32_t* ctl, int b, float& inv_t, uint64_t& seed) {
+  inv_t = ctl ? __uint_as_float(ctl[3 * b]) : 0.f;
+  seed = ctl ? ((uint64_t)ctl[3 * b + 2] << 32 | ctl[3 * b + 1]) : 0ull;
 }
 
 // block (256 threads) argmax with lowest-id ties, result broadcast to thread 0's registers
@@ -342,7 +345,7 @@ __device__ __forceinline__ void greedy_scan(const SelP& p, const E* row, int b, 
     if (x > -INFINITY) {
       if (lse) lse_add(a.m, a.se, x);
       if (sample) {
-        const float g = x * inv_t + gumbel(seed, b, p.col, v);
+        const float g = x * inv_t + gumbel(seed, 0, p.col, v);
         if (g > a.sbest || (g == a.sbest && v < a.sbesti)) { a.sbest = g; a.sbesti = v; }
       }
     }
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(SelP p, int slice, f
   sel_prologue(p);
   float inv_t;
   uint64_t seed;
-  read_ctl(p.ctl, inv_t, seed);
+  read_ctl(p.ctl, b, inv_t, seed);
   const bool sample = inv_t > 0.f, lse = p.sum_logp != nullptr;
   const E* row = (const E*)p.logits + b * p.ld;
   GreedyAcc a;
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(64) void greedy_merge_kernel(SelP p, int G, const f
   sel_prologue(p);
   float inv_t;
   uint64_t seed;
-  read_ctl(p.ctl, inv_t, seed);
+  read_ctl(p.ctl, b, inv_t, seed);
   const bool sample = inv_t > 0.f, lse = p.sum_logp != nullptr;
   GreedyAcc a;
   greedy_init(a);
@@ -531,7 +534,7 @@ __device__ __forceinline__ void ts_finish(const SelTsP& q, const TsRow& r, int b
   const int tid = threadIdx.x;
   float inv_t;
   uint64_t seed;
-  read_ctl(p.ctl, inv_t, seed);
+  read_ctl(p.ctl, b, inv_t, seed);
   const bool sample = inv_t > 0.f;
   const E* row = (const E*)p.logits + b * p.ld;
   if (tid == 0) {
@@ -545,7 +548,7 @@ __device__ __forceinline__ void ts_finish(const SelTsP& q, const TsRow& r, int b
     float sb = -INFINITY;
     for_row(p, row, [&](int v, float x, bool sup, bool beg) {
       if (ts_masked(q, r, v, sup, beg) || !(x > -INFINITY) || (mask_text && v < q.ts_begin)) return;
-      const float g = x * inv_t + gumbel(seed, b, p.col, v);
+      const float g = x * inv_t + gumbel(seed, 0, p.col, v);
       if (g > sb || (g == sb && v < spick)) { sb = g; spick = v; }
     });
     block_argmax(sb, spick, sx, sxi, 2);

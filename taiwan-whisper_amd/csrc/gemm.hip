@@ -393,7 +393,7 @@ __device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v
   if (flags & F_DGELU) v = rnd<H>(v * gelu_erf_grad(e2f<H>(p.aux[(int64_t)m * p.ldaux + n])));
   if (flags & F_GELU) {
     if (flags & F_AUX_OUT) p.aux[(int64_t)m * p.ldaux + n] = f2e<H>(v);
-    v = rnd<H>(gelu_erf(v));
+    v = rnd<H>(gelu_of<H>(v));
   }
   if (flags & F_RES) {
     const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
@@ -565,12 +565,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
 #pragma unroll
     for (int u = 0; u < GV_PRE; ++u) wpre[c][u] = (u < npre) ? *(const bf16x8*)(wr + lane * 8 + u * 512) : bf16x8{};
   }
-  if (wave < MR) {
-    bf16* dst = xs + (int64_t)wave * K;
-    if (wave >= p.M) {
+  // wave w stages rows w, w + 4 (MR = 8: the batched-fallback decode of up to 8 rows)
+  for (int row = wave; row < MR; row += 4) {
+    bf16* dst = xs + (int64_t)row * K;
+    if (row >= p.M) {
       for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = bf16x8{};
     } else if (lnw) {
-      const bf16* xr = p.A + (int64_t)wave * p.lda;
+      const bf16* xr = p.A + (int64_t)row * p.lda;
       const int hl = lane & 31, nch = K / 256;
       float s = 0.f;
       for (int c = 0; c < nch; ++c) {
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
         }
       }
     } else {
-      const bf16* xr = p.A + (int64_t)wave * p.lda;
+      const bf16* xr = p.A + (int64_t)row * p.lda;
       for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = *(const bf16x8*)(xr + e);
     }
   }
@@ -1122,14 +1123,15 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   } else if (flags & F_CLAMP16) {
     return TW_EINVAL;
   }
-  if (M > 4 || K <= 0 || (K % 8) || (ldx % 8) || (ldw % 8)) return TW_EINVAL;
+  if (M > 8 || K <= 0 || (K % 8) || (ldx % 8) || (ldw % 8)) return TW_EINVAL;
   if (((uintptr_t)x & 15) || ((uintptr_t)W & 15)) return TW_EINVAL;
   if (ln_w && (!ln_b || (K % 256) || (((uintptr_t)ln_w | (uintptr_t)ln_b) & 15))) return TW_EINVAL;
   if ((flags & F_BIAS) && !bias) return TW_EINVAL;
   if ((flags & F_RES) && !res) return TW_EINVAL;
   if ((flags & (F_AUX_OUT | F_DGELU)) && !aux) return TW_EINVAL;
   if (c_dtype != TW_F32 && c_dtype != TW_BF16) return TW_EUNSUPPORTED;
-  if ((size_t)4 * K * 2 > 64 * 1024) return TW_EUNSUPPORTED;        // A rows in LDS
+  const int mr = M == 1 ? 1 : M == 2 ? 2 : M <= 4 ? 4 : 8;
+  if ((size_t)mr * K * 2 > 80 * 1024) return TW_EUNSUPPORTED;        // A rows in LDS
   if (kv_cache && (!t_dev || kv_col0 < 0 || kv_col0 >= N)) return TW_EINVAL;
   const GemvKV kv{kv_cache, kv_sb, kv_ld, kv_col0, t_dev};
   GemmP p = {};
@@ -1141,21 +1143,24 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   // one output column per wave, or 8 for very wide N (the LM head: fewer workgroups repeating the A prologue)
   const int cpw = N >= 16384 ? 8 : 1;
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
-  const size_t lds = (size_t)(M == 1 ? 1 : M == 2 ? 2 : 4) * K * 2;
+  const size_t lds = (size_t)mr * K * 2;
 #define TW_GEMV(MR_, CPW_, PRE_) \
   hipLaunchKernelGGL((gemv_kernel<H, MR_, CPW_, PRE_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
   if (cpw == 8) {
-    if (M == 1) TW_GEMV(1, 8, 3);
-    else if (M == 2) TW_GEMV(2, 8, 3);
-    else TW_GEMV(4, 8, 3);
+    if (mr == 1) TW_GEMV(1, 8, 3);
+    else if (mr == 2) TW_GEMV(2, 8, 3);
+    else if (mr == 4) TW_GEMV(4, 8, 3);
+    else TW_GEMV(8, 8, 3);
   } else if (K <= 1536) {
-    if (M == 1) TW_GEMV(1, 1, 3);
-    else if (M == 2) TW_GEMV(2, 1, 3);
-    else TW_GEMV(4, 1, 3);
+    if (mr == 1) TW_GEMV(1, 1, 3);
+    else if (mr == 2) TW_GEMV(2, 1, 3);
+    else if (mr == 4) TW_GEMV(4, 1, 3);
+    else TW_GEMV(8, 1, 3);
   } else {
-    if (M == 1) TW_GEMV(1, 1, 10);
-    else if (M == 2) TW_GEMV(2, 1, 10);
-    else TW_GEMV(4, 1, 10);
+    if (mr == 1) TW_GEMV(1, 1, 10);
+    else if (mr == 2) TW_GEMV(2, 1, 10);
+    else if (mr == 4) TW_GEMV(4, 1, 10);
+    else TW_GEMV(8, 1, 10);
   }
 #undef TW_GEMV
   TW_CHECK_LAUNCH();

@@ -206,7 +206,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
             *(bf16x4*)(p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n) =
                 bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = rnd<H>(gelu_erf(v[r]));
+          for (int r = 0; r < 4; ++r) v[r] = rnd<H>(gelu_of<H>(v[r]));
         }
         if (flags & (F_RES | F_ACCUM)) {
 #pragma unroll
@@ -253,7 +253,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
           for (int r = 0; r < nv; ++r) ax[r] = f2e<H>(v[r]);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = rnd<H>(gelu_erf(v[r]));
+        for (int r = 0; r < 4; ++r) v[r] = rnd<H>(gelu_of<H>(v[r]));
       }
       if (flags & F_RES) {
         const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
@@ -408,9 +408,14 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int r = 0; r < 4; r += 2) {
-            const f32x2 y = gelu_erf2(f32x2{v[h][r], v[h][r + 1]});
-            v[h][r] = y.x;
-            v[h][r + 1] = y.y;
+            if constexpr (H) {
+              v[h][r] = gelu_of<H>(v[h][r]);
+              v[h][r + 1] = gelu_of<H>(v[h][r + 1]);
+            } else {
+              const f32x2 y = gelu_erf2(f32x2{v[h][r], v[h][r + 1]});
+              v[h][r] = y.x;
+              v[h][r + 1] = y.y;
+            }
           }
         bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
         *(u32x4*)(crow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);

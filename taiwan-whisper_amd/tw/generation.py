@@ -69,25 +69,37 @@ class DecodeSession:
         self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=act, device=dev)
         self.logits = torch.empty(B, model.Vp, dtype=act, device=dev)
         self.graph = None
-        # batch <= 4 on the bf16 path: every Linear is one tw_gemv_bf16 launch, with the LayerNorm in front
-        # of it fused when the residual stream is bf16 (bit-identical A); larger batches use the skinny
-        # GEMM with a separate LayerNorm
-        self.gemv = B <= 4 and model.compute in ("bf16", "fp16") and d % 256 == 0
+        # batch <= 8 on the bf16 / fp16 paths: every Linear is one GEMV launch, with the LayerNorm in front of it
+        # fused when the residual stream is 16-bit (bit-identical A); larger batches use the skinny GEMM with a
+        # separate LayerNorm
+        self.gemv = B <= 8 and model.compute in ("bf16", "fp16") and d % 256 == 0
         self.gemv_ln = self.gemv and model.stream_dtype == act
 
     def set_encoder(self, enc16):
-        """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe)."""
+        """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe).  enc16 holds B*Tk
+        rows, or Tk rows shared by every row of the batch (the speculative fallback batch of one window: the
+        K/V are projected once and copied, so each row sees exactly the K/V of a batch-1 decode)."""
         m, d = self.m, self.d
+        shared = enc16.shape[0] == self.Tk and self.B > 1
+        nb = 1 if shared else self.B
         # head-major: the projection goes through one [B*Tk][2d] scratch block that lives only for this call
         # (3.9 GB at the 512-clip large-v2 batch; the caching allocator reuses it for the next window)
-        proj = torch.empty(self.B * self.Tk, 2 * d, dtype=m.act_dtype, device=m.device) if self.hm else None
+        proj = torch.empty(nb * self.Tk, 2 * d, dtype=m.act_dtype, device=m.device) if self.hm or shared else None
         for i, kv in enumerate(self.cross_kv):
             p = f"model.decoder.layers.{i}.encoder_attn"
             wkv = m.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
             bkv = m.wspan(p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
-            if self.hm:
+            if self.hm and shared:               # K [B][H][Tk][64] then V: one clip's blocks, copied to every row
                 m._lin(enc16, wkv, bkv, proj)
-                F.kv_head_major(proj, 2 * d, kv, self.B, self.Tk, self.H)
+                one = torch.empty(2 * self.H * self.Tk * 64, dtype=m.act_dtype, device=m.device)
+                F.kv_head_major(proj, 2 * d, one, 1, self.Tk, self.H)
+                kv.view(2, self.B, -1).copy_(one.view(2, 1, -1).expand(-1, self.B, -1))
+            elif self.hm:
+                m._lin(enc16, wkv, bkv, proj)
+                F.kv_head_major(proj, 2 * d, kv, nb, self.Tk, self.H)
+            elif shared:
+                m._lin(enc16, wkv, bkv, proj)
+                kv.view(self.B, self.Tk, 2 * d).copy_(proj.view(1, self.Tk, 2 * d).expand(self.B, -1, -1))
             else:
                 m._lin(enc16, wkv, bkv, kv)
         del proj
@@ -223,20 +235,25 @@ class _Select:
         self.no_ts = int(gc.no_timestamps_token_id)
         mi = gc.max_initial_timestamp_index if "max_initial_timestamp_index" in gc else None
         self.max_initial = -1 if mi is None else int(mi)
-        # temperature fallback: sampling control word (1/T, seed) read on the device, so a captured
-        # graph serves every temperature; running log-prob of the chosen tokens
-        self.ctl = torch.zeros(3, dtype=torch.int32, device=dev) if track else None
+        # temperature fallback: one sampling control word (1/T, seed) per row, read on the device, so a captured
+        # graph serves every temperature and the rows of a batch can be different fallback attempts; running
+        # log-prob of the chosen tokens
+        self.B = B
+        self.ctl = torch.zeros(3 * B, dtype=torch.int32, device=dev) if track else None
         self.sum_logp = torch.zeros(B, dtype=torch.float32, device=dev) if track else None
 
     def reset(self, prompt, temperature=0.0, seed=0):
+        """temperature / seed: one value for every row, or one per row."""
         self.ids.fill_(self.eos)
         self.ids[:, :self.P] = prompt
         self.done.zero_()
         self.last_ts.fill_(-1)
+        temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature] * self.B
+        seeds = list(seed) if isinstance(seed, (list, tuple)) else [seed] * self.B
         if self.track:
             self.sum_logp.zero_()
-            F.sample_ctl(temperature, seed, self.ctl)
-        elif temperature:
+            F.sample_ctl(temps, seeds, self.ctl)
+        elif any(temps):
             raise ValueError("sampling needs a tracking selector (track=True)")
 
     def __call__(self, sess):
@@ -367,7 +384,7 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     window = 2 * cfg.max_source_positions                     # 3000 feature frames = 30 s
     if encoder_outputs is None and input_features is not None and input_features.shape[-1] > window:
         return _longform(model, gc, input_features, attention_mask, language, task, max_length, max_new_tokens,
-                         use_graph, window, kw.get("_trace"), **fb)
+                         use_graph, window, kw.get("_trace"), fallback_batch=bool(kw.get("fallback_batch", True)), **fb)
     if kw.get("do_sample") or fb["temperature"] not in (0, 0.0) or fb["logprob_threshold"] is not None \
             or fb["compression_ratio_threshold"] is not None or fb["no_speech_threshold"] is not None:
         # the reference applies fallback / thresholds to long-form inputs only (run_eval.py:659-685)
@@ -424,7 +441,7 @@ def need_fallback(tokens, avg_logprob, no_speech_prob, vocab_size, compression_r
 
 def _longform(model, gc, feats, attention_mask, language, task, max_length, max_new_tokens, use_graph, window,
               trace=None, temperature=0.0, compression_ratio_threshold=None, logprob_threshold=None,
-              no_speech_threshold=None, condition_on_prev_tokens=False, seed=0):
+              no_speech_threshold=None, condition_on_prev_tokens=False, seed=0, fallback_batch=True):
     """HF sequential long-form generate (generation_whisper.py step 6): per input, 30 s windows from
     `seek`; each window decoded with timestamp rules at the first temperature of `temperature` and
     re-decoded at the next one while HF's fallback test fails (compression ratio of the token bytes,
@@ -436,7 +453,9 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
     segment's closing timestamp of a double-timestamp ending dropped) + the task prompt.  Returns
     the concatenated segment tokens, right-padded with pad.  Sampled windows draw from
     softmax(x / T) with the engine's counter-based RNG (seeded by `seed`, the clip, the window and
-    the fallback index), not torch's RNG stream."""
+    the fallback index), not torch's RNG stream.  Once a window's first attempt fails, the remaining
+    temperatures are decoded together as one batch (fallback_batch; identical tokens and gates to decoding
+    them one by one, see the loop below)."""
     cfg = model.config
     dev = model.device
     feats = feats.to(dev, torch.float32)
@@ -457,10 +476,19 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
         prev_sot = sup[-2] if len(sup) >= 2 else None
     decoders = {}
 
-    def decoder(P, ml):
-        if (P, ml) not in decoders:
-            decoders[(P, ml)] = _Decoder(model, gc, 1, cfg.max_source_positions, P, ml, True, use_graph, track)
-        return decoders[(P, ml)]
+    def decoder(P, ml, nb=1):
+        if (P, ml, nb) not in decoders:
+            decoders[(P, ml, nb)] = _Decoder(model, gc, nb, cfg.max_source_positions, P, ml, True, use_graph, track)
+        return decoders[(P, ml, nb)]
+
+    def trim(raw):
+        cand = list(raw)
+        if cand and cand[-1] == pad:                     # HF: padding removed except one eos
+            k = len(cand)
+            while k > 1 and cand[k - 2] == pad:
+                k -= 1
+            cand = cand[:k] if pad == eos else cand[:k - 1]
+        return cand
 
     seg_in = torch.zeros(1, nmel, window, dtype=torch.float32, device=dev)
     outs = []
@@ -487,31 +515,48 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
             ptens = torch.tensor([prompt], dtype=torch.int64, device=dev)
             ns = (P - len(init), ns_token) if no_speech_threshold is not None else None
             skip, t_acc, seq = False, temps[0], []
-            for fi, temp in enumerate(temps):
-                raw = dec.run(enc16, ptens, temperature=temp or 0.0,
-                              seed=(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1),
-                              no_speech=ns)[0].tolist()
-                cand = list(raw)
-                if cand and cand[-1] == pad:                     # HF: padding removed except one eos
-                    k = len(cand)
-                    while k > 1 and cand[k - 2] == pad:
-                        k -= 1
-                    cand = cand[:k] if pad == eos else cand[:k - 1]
-                needs = False
-                if track or compression_ratio_threshold is not None:
-                    tg = time.perf_counter()          # gate cost: log-prob / no-speech readback + compression ratio
-                    avg = float(dec.sel.sum_logp[0]) / max(len(cand), 1) if track else 0.0
-                    nsp = float(torch.exp(dec.ns_logp[0])) if ns is not None else 0.0
-                    needs, skip = need_fallback(cand, avg, nsp, V, compression_ratio_threshold, logprob_threshold,
-                                                no_speech_threshold)
-                    if trace is not None:
-                        trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw),
-                                          avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip,
-                                          gate_ms=(time.perf_counter() - tg) * 1e3))
-                elif trace is not None:
-                    trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw)))
-                seq, t_acc = raw, temp
-                if not needs:
+            # attempt fi draws with seed(fi); attempts 1.. run as ONE batch (one row per remaining temperature,
+            # speculatively) once attempt 0 fails its gate: a batch-1 decode step is launch-bound, so the
+            # batch costs about what one attempt does.  Rows are independent (per-row temperature / seed,
+            # tw_select_sample_ts), so each row decodes exactly the tokens its sequential attempt would, and the
+            # first passing row in temperature order is accepted, as HF generate_with_fallback accepts it.
+            seeds = [(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1) for fi in range(len(temps))]
+            attempts = [(0, dec, enc16, ptens, [temps[0] or 0.0], [seeds[0]])]
+            rest = list(range(1, len(temps)))
+            per = 8 if fallback_batch else 1                 # fallback_batch=False: one attempt at a time (A/B, tests)
+            for fb in range(0, len(rest), per):
+                grp = rest[fb:fb + per]
+                attempts.append((grp[0], None, None, None, [temps[f] or 0.0 for f in grp], [seeds[f] for f in grp]))
+            for fi0, d_, e_, p_, tl, sl in attempts:
+                if d_ is None:                               # a speculative batch of the remaining attempts
+                    nb = len(tl)
+                    d_ = decoder(P, ml, nb)
+                    e_ = enc16                               # shared by the rows (DecodeSession.set_encoder)
+                    p_ = ptens.repeat(nb, 1)
+                raws = d_.run(e_, p_, temperature=tl if len(tl) > 1 else tl[0], seed=sl if len(sl) > 1 else sl[0],
+                              no_speech=ns).tolist()
+                done_here = False
+                for r, raw in enumerate(raws):
+                    fi, temp = fi0 + r, temps[fi0 + r]
+                    cand = trim(raw)
+                    needs = False
+                    if track or compression_ratio_threshold is not None:
+                        tg = time.perf_counter()      # gate cost: log-prob / no-speech readback + compression ratio
+                        avg = float(d_.sel.sum_logp[r]) / max(len(cand), 1) if track else 0.0
+                        nsp = float(torch.exp(d_.ns_logp[r])) if ns is not None else 0.0
+                        needs, skip = need_fallback(cand, avg, nsp, V, compression_ratio_threshold, logprob_threshold,
+                                                    no_speech_threshold)
+                        if trace is not None:
+                            trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw),
+                                              avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip,
+                                              batch=len(raws), gate_ms=(time.perf_counter() - tg) * 1e3))
+                    elif trace is not None:
+                        trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw)))
+                    seq, t_acc = raw, temp
+                    if not needs:
+                        done_here = True
+                        break
+                if done_here:
                     break
             nwin += 1
             cond = bool(condition_on_prev_tokens) and (t_acc is None or t_acc < 0.5)

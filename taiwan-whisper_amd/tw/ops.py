@@ -97,13 +97,13 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
 
 
 def gemv(x, W, C, *, ln_w=None, ln_b=None, eps=1e-5, bias=None, res=None, aux=None, flags=0, kv=None):
-    """tw_gemv_bf16: C[m] = epi(A[m] . W^T) for M <= 4 rows, A = x or LayerNorm(x) (ln_w / ln_b given):
+    """tw_gemv_bf16 / tw_gemv_f16: C[m] = epi(A[m] . W^T) for M <= 8 rows, A = x or LayerNorm(x) (ln_w / ln_b given):
     the batch-1 decode step's LN + Linear pairs in one launch (include/tw_hip.h).  kv = (cache, sb, ld, col0,
     t_dev, t_max): columns >= col0 also go to cache row *t_dev (the fused KV append)."""
     M, K = x.shape
     N = W.shape[0]
     h = x.dtype
-    assert h in HALF and W.dtype == h and M <= 4 and W.shape[1] == K
+    assert h in HALF and W.dtype == h and M <= 8 and W.shape[1] == K
     assert x.stride(1) == 1 and W.is_contiguous()
     _need(C, (M - 1) * C.stride(0) + N, "gemv C")
     if ln_w is not None:
@@ -431,9 +431,9 @@ def greedy_select_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids
 
 def select_sample(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos, done, ids, col, next_ids, ctl,
                   sum_logp, t_dev=None, begin_col=-1):
-    """greedy_select + temperature sampling (ctl: int32[3] = bits(1/T), seed lo, hi; 1/T = 0 -> argmax)
+    """greedy_select + temperature sampling (ctl: int32[3B], per row bits(1/T), seed lo, hi; 1/T = 0 -> argmax)
     + running log-prob of the chosen token (sum_logp: float32[B])."""
-    assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
+    assert ctl.dtype == torch.int32 and ctl.numel() >= 3 * B and sum_logp.dtype == torch.float32
     _need(sum_logp, B, "select sum_logp")
     assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and ids.dtype == torch.int64
     assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8
@@ -447,7 +447,7 @@ def select_sample(logits, ld, B, V, suppress_bits, begin_bits, apply_begin, eos,
 
 def select_sample_ts(logits, ld, B, V, suppress_bits, begin_bits, eos, done, ids, col, next_ids, last_ts, begin_col,
                      ctl, sum_logp, ts_begin=50364, no_ts=50363, max_initial=-1, t_dev=None):
-    assert ctl.dtype == torch.int32 and ctl.numel() >= 3 and sum_logp.dtype == torch.float32
+    assert ctl.dtype == torch.int32 and ctl.numel() >= 3 * B and sum_logp.dtype == torch.float32
     _need(sum_logp, B, "select sum_logp")
     assert logits.dtype in (torch.bfloat16, torch.float16, torch.float32) and ids.dtype == torch.int64
     assert next_ids.dtype == torch.int64 and done.dtype == torch.uint8 and last_ts.dtype == torch.int32
@@ -468,18 +468,25 @@ def token_logprob(logits, ld, B, V, token, out):
     return out
 
 
-def sample_ctl(temperature: float, seed: int, out=None):
-    """Device control word of select_sample[_ts]: [bits(1/T) (0 = greedy), seed lo, seed hi]."""
+def sample_ctl(temperature, seed, out=None):
+    """Device control words of select_sample[_ts], one per row: [bits(1/T) (0 = greedy), seed lo, seed hi] x B.
+    temperature / seed: scalars (one row) or equal-length sequences (a batch of independent attempts)."""
     import struct
-    inv = 0.0 if not temperature or temperature <= 0 else 1.0 / float(temperature)
-    bits = struct.unpack("<i", struct.pack("<f", inv))[0]
-    seed = int(seed) & ((1 << 64) - 1)
-    lo, hi = seed & 0xFFFFFFFF, seed >> 32
-    vals = torch.tensor([bits, lo - (1 << 32) if lo >= 1 << 31 else lo, hi - (1 << 32) if hi >= 1 << 31 else hi],
-                        dtype=torch.int32)
+    temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
+    seeds = list(seed) if isinstance(seed, (list, tuple)) else [seed] * len(temps)
+    assert len(seeds) == len(temps)
+    vals = []
+    for t, sd in zip(temps, seeds):
+        inv = 0.0 if not t or t <= 0 else 1.0 / float(t)
+        bits = struct.unpack("<i", struct.pack("<f", inv))[0]
+        sd = int(sd) & ((1 << 64) - 1)
+        lo, hi = sd & 0xFFFFFFFF, sd >> 32
+        vals += [bits, lo - (1 << 32) if lo >= 1 << 31 else lo, hi - (1 << 32) if hi >= 1 << 31 else hi]
+    vals = torch.tensor(vals, dtype=torch.int32)
     if out is None:
         return vals
-    out.copy_(vals)
+    assert out.numel() >= vals.numel()
+    out[:vals.numel()].copy_(vals)
     return out
 
 

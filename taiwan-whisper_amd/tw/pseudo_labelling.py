@@ -53,7 +53,8 @@ def parse_args(argv=None):
     ap.add_argument("--model_size_or_path", type=str, default="tiny",
                     help="HF-format model directory (config.json + model.safetensors)")
     ap.add_argument("--compute_type", type=str, default="default",
-                    help="default / bfloat16 / float16 -> bf16 autocast path; float32 -> the fp32 path")
+                    help="default / float16 -> the fp16 model (CTranslate2's CUDA default for a float16 checkpoint); "
+                         "bfloat16 -> bf16; float32 -> the fp32 path")
     ap.add_argument("--chunk_length", type=int, default=5)
     ap.add_argument("--batch_size", type=int, default=64)
     ap.add_argument("--num_workers", type=int, default=8, help="host audio-decoding threads")
@@ -226,10 +227,11 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    compute = "fp32" if args.compute_type in ("float32", "fp32") else "bf16"
+    ct = args.compute_type
+    compute = "fp32" if ct in ("float32", "fp32") else "bf16" if ct in ("bfloat16", "bf16") else "fp16"
+    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[compute]
     model = WhisperForConditionalGeneration.from_pretrained(
-        args.model_size_or_path, torch_dtype=torch.float32 if compute == "fp32" else torch.bfloat16,
-        device=torch.device("cuda", local), compute=compute)
+        args.model_size_or_path, torch_dtype=dtype, device=torch.device("cuda", local), compute=compute)
     print(f"Using device: cuda:{local} ({compute})", flush=True)
     decode = load_text_decoder(args)
     tr = ChunkTranscriber(model, args.language, args.max_new_tokens)

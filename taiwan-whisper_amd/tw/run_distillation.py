@@ -192,8 +192,10 @@ def teacher_dtype(dtype: str):
         if not fp32_compute_supported():
             raise NotImplementedError("--dtype float32 (mixed_precision='no') needs the fp32 arithmetic path")
         return torch.float32
-    raise NotImplementedError(f"--dtype {dtype}: only bfloat16 and float32 are implemented (fp16 autocast "
-                              "with a dynamic loss scaler is not)")
+    raise NotImplementedError(f"--dtype {dtype}: distillation trains in bfloat16 or float32 (every reference "
+                              "launcher uses bfloat16); fp16 autocast with a dynamic loss scaler is not implemented. "
+                              "fp16 INFERENCE (torch_dtype=float16: run_eval.py / pseudo-labelling) is: "
+                              "WhisperForConditionalGeneration.from_pretrained(dir, torch_dtype=torch.float16)")
 
 
 def load_models(args, device, tokenizer=None):

@@ -58,7 +58,8 @@ def test_sampling_kernel_distribution_and_logprob(T):
     ids = torch.zeros(B, 4, dtype=torch.int64, device="cuda")
     done = torch.zeros(B, dtype=torch.uint8, device="cuda")
     nxt = torch.zeros(B, dtype=torch.int64, device="cuda")
-    ctl = F.sample_ctl(T, 1234).cuda()
+    # one control word per row (each row an independent attempt with its own seed)
+    ctl = F.sample_ctl([T] * B, [1234 + 7919 * b for b in range(B)]).cuda()
     slp = torch.zeros(B, dtype=torch.float32, device="cuda")
     F.select_sample(logits, V, B, V, F.token_bitmask(sup, V, "cuda"), None, False, 50257 % V, done, ids, 1, nxt, ctl,
                     slp)
@@ -74,7 +75,7 @@ def test_sampling_kernel_distribution_and_logprob(T):
     lp = torch.log_softmax(xm, -1)
     np.testing.assert_allclose(slp.cpu().numpy(), lp[tok].numpy(), atol=1e-4)
     # greedy (1/T = 0) through the same kernel: argmax, same log-prob rule
-    F.sample_ctl(0.0, 0, ctl)
+    F.sample_ctl([0.0] * B, [0] * B, ctl)
     slp.zero_(); done.zero_()
     F.select_sample(logits, V, B, V, F.token_bitmask(sup, V, "cuda"), None, False, 50257 % V, done, ids, 2, nxt, ctl,
                     slp)
@@ -82,7 +83,7 @@ def test_sampling_kernel_distribution_and_logprob(T):
     assert bool((ids[:, 2].cpu() == int(xm.argmax())).all())
     np.testing.assert_allclose(slp.cpu().numpy(), float(lp.max()), atol=1e-4)
     # a different seed gives a different draw sequence
-    F.sample_ctl(T, 99, ctl)
+    F.sample_ctl([T] * B, [99 + 7919 * b for b in range(B)], ctl)
     F.select_sample(logits, V, B, V, None, None, False, 50257 % V, done.zero_(), ids, 3, nxt, ctl, slp)
     torch.cuda.synchronize()
     assert not torch.equal(ids[:, 3].cpu(), tok)
@@ -103,7 +104,7 @@ def test_sampling_respects_timestamp_rules():
     done = torch.zeros(B, dtype=torch.uint8, device="cuda")
     nxt = torch.zeros(B, dtype=torch.int64, device="cuda")
     last_ts = torch.full((B,), -1, dtype=torch.int32, device="cuda")
-    ctl = F.sample_ctl(1.0, 3).cuda()
+    ctl = F.sample_ctl([1.0] * B, [3 + 7919 * b for b in range(B)]).cuda()
     slp = torch.zeros(B, dtype=torch.float32, device="cuda")
     F.select_sample_ts(logits, 51904, B, V, None, None, 50257, done, ids, 3, nxt, last_ts, 3, ctl, slp,
                        max_initial=10)
@@ -241,3 +242,26 @@ def test_sampled_fallback_control_flow():
         toks = t["raw"]
         assert toks[0] >= 50364 and toks[0] <= 50364 + 50           # first step: a timestamp <= max_initial
         assert 50363 not in toks
+
+
+def test_batched_fallback_equals_sequential():
+    """The speculative fallback batch (after a window's first attempt fails, the remaining temperatures decode
+    together as one batch, one row per temperature with its own seed) gives exactly the attempts of decoding
+    them one at a time: the same sampled tokens, the same per-attempt average log-prob and no-speech
+    probability, the same accepted attempt and output (tw/generation.py _longform)."""
+    mg, cfg, w, m = _setup()
+    lf = torch.from_numpy(mg.longform_features())
+    kw = dict(attention_mask=torch.ones(1, lf.shape[-1], dtype=torch.long), return_timestamps=True, language="zh",
+              task="transcribe", temperature=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0), compression_ratio_threshold=1.35,
+              logprob_threshold=-1.0, no_speech_threshold=0.6, max_new_tokens=40, seed=5)
+    ta, tb = [], []
+    a = m.generate(lf, _trace=ta, fallback_batch=True, **kw).cpu()[0].tolist()
+    b = m.generate(lf, _trace=tb, fallback_batch=False, **kw).cpu()[0].tolist()
+    assert a == b
+    assert len(ta) == len(tb) and any(t["batch"] > 1 for t in ta)
+    strip = lambda r: r[:next((i + 1 for i, x in enumerate(r) if x == 50257), len(r))]
+    for x, y in zip(ta, tb):
+        assert (x["seek"], x["T"], x["prompt"]) == (y["seek"], y["T"], y["prompt"])
+        assert strip(x["raw"]) == strip(y["raw"])
+        assert x["avg_logprob"] == y["avg_logprob"] and x["no_speech_prob"] == y["no_speech_prob"]
+        assert (x["needs_fallback"], x["skip"]) == (y["needs_fallback"], y["skip"])

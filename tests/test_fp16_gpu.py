@@ -10,7 +10,8 @@ End to end against HF Transformers run with torch_dtype=float16 (tests/golden/fp
   * micro forward: encoder output and logits within 2 / 4 fp16 ulps of the row scale;
   * greedy ids, timestamp ids (one window and 65 s long-form) and the conditioned long-form: IDENTICAL to HF
     fp16 generate (no near-tie allowance);
-  * per-window average log-probs within two fp16 ulps of the logit scale (2^-7), no-speech within 1e-2 rel.
+  * per-window average log-probs within 5e-3 of the fp16 oracle teacher-forced along the same tokens and within
+    2e-2 of HF (the fp16 sequence-order noise floor, measured on the oracle itself), no-speech within 1e-2 rel.
 """
 import os
 import sys
@@ -89,16 +90,18 @@ def test_gemm_f16_gelu_residual_clamp():
     assert float(_ulps(pre.float(), y, mag).max()) <= 1.0
     gelu = _h(torch.nn.functional.gelu(pre.float()))           # GELU of the kernel's own pre-activation
     assert float(_ulps(H.float(), gelu).max()) <= 1.0
-    # residual + the encoder clamp: rows of large residuals saturate at fp16(64504) = 64512, as torch.clamp
+    # residual + the encoder clamp, in place: HF's `residual + hidden_states` of two fp16 tensors (one rounding of
+    # the exact sum) then clamp(+-64504) -> fp16(64504) = 64512; the Linear output is the kernel's own (no residual)
+    P = torch.empty(M, N, device=DEV, dtype=torch.float16)
+    ops.gemm(A, W, P, M, N, K, lda=K, ldb=K, ldc=N, bias=b, flags=ops.GEMM_ROUND)
     res = torch.randn(M, N, device=DEV, generator=g).half()
     res[:8] = 65000.0
     res[8:16] = -65500.0
     X = res.clone()
     ops.gemm(A, W, X, M, N, K, lda=K, ldb=K, ldc=N, bias=b, res=X, ldr=N, flags=ops.GEMM_ROUND | ops.GEMM_CLAMP16)
-    want = (y + res.float()).half().float().clamp(-64504.0, 64504.0).half().float()
-    assert torch.isfinite(X.float()).all()
-    assert float(_ulps(X.float()[16:], want[16:], mag[16:] + res.float()[16:].abs()).max()) <= 1.0
-    assert (X.float()[:16].abs() <= 64512.0).all() and (X.float()[:8] > 60000).all()
+    want = (P.float() + res.float()).half().float().clamp(-64504.0, 64504.0).half()
+    assert torch.equal(X, want)
+    assert torch.isfinite(X.float()).all() and (X.float()[:8] > 60000).all() and (X.float()[:16].abs() <= 64512).all()
 
 
 def test_gemv_f16_layernorm_matches_ln_then_gemm():
@@ -240,37 +243,40 @@ def test_fp16_timestamps_longform_fallback_vs_hf():
     trace = []
     m.generate(lf, temperature=(0.0,), logprob_threshold=-1e9, no_speech_threshold=1.0, _trace=trace, **kw)
     np.testing.assert_allclose([t["no_speech_prob"] for t in trace], h["f16_fb_ns_probs"], rtol=1e-2)
-    # average log-prob: within two fp16 ulps of the logit scale (2^-7), unless the window holds a step whose
-    # WhisperTimeStampLogitsProcessor "timestamp mass beats every text token" test is itself a near-tie (within
-    # 4 fp16 ulps): the chosen token is the same either way (the ids above are identical), but the branch decides
-    # whether text tokens enter the log-softmax normaliser, which moves that step's log-prob by >= log 2 (HF's
-    # own fp32 and fp16 runs differ by 0.77 on window 2 for exactly this reason: fallback.npz vs fp16.npz)
-    for i, (t, want) in enumerate(zip(trace, h["f16_fb_avg_logprobs"])):
-        if abs(t["avg_logprob"] - want) <= 2.0 ** -7:
-            continue
-        margin = _mass_margin(m, lf, t)
-        assert margin <= 4 * 2.0 ** -10 * 4, (i, t["avg_logprob"], want, margin)
+    # average log-prob over the window's (here 445) tokens.  Against HF: 2e-2.  The fp16 stream makes this mean
+    # sensitive to the ORDER of fp32 reductions (one-ulp flips of fp16 activations compound through the layers):
+    # the fp16 oracle itself, decoding free-running (the CPU pin, tests/test_oracle_golden.py) and teacher-forced
+    # along the same tokens, differs by 1.1e-2 on window 2.  Against that teacher-forced oracle along the
+    # engine's own tokens (the same arithmetic; the engine decodes incrementally, so the same order noise applies,
+    # measured 0.8-2.4e-3): 5e-3.
+    np.testing.assert_allclose([t["avg_logprob"] for t in trace], h["f16_fb_avg_logprobs"], rtol=0, atol=2e-2)
+    for t in trace:
+        assert abs(t["avg_logprob"] - _oracle_avg(lf, t)) <= 5e-3
 
 
-def _mass_margin(m, lf, t):
-    """min over the window's steps of |logsumexp(timestamp logits) - max(text logit)| after the other timestamp
-    rules, from the engine's own teacher-forced fp16 logits."""
-    from oracle.greedy_ref import timestamp_rules
+def _oracle_avg(lf, t):
+    """The window's average log-prob from the fp16 oracle (CPU), teacher-forced along the engine's tokens."""
+    from oracle import greedy_ref
+    from oracle.weights import CONFIGS, make_weights
+    from oracle.whisper_ref import Ref, to_torch
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
     import make_golden as mg
+    cfg = CONFIGS["micro"]
+    ref = Ref(cfg, to_torch(make_weights(cfg, 1, lin_std=0.2), torch.float16), amp=True, stream_bf16=True,
+              half=torch.float16)
     seg = torch.zeros(1, 80, 3000)
     seg[0, :, :t["n"]] = lf[0, :, t["seek"]:t["seek"] + t["n"]]
     raw, P = list(t["raw"]), len(t["prompt"])
-    dec = torch.tensor([t["prompt"] + raw[:-1]], device=DEV)
-    lg = m(input_features=seg.to(DEV), decoder_input_ids=dec).logits[0].float().cpu()
-    best = float("inf")
-    for i in range(len(raw)):
-        row = lg[P - 1 + i].clone()
+    with torch.no_grad():
+        lg = ref.forward(seg, torch.tensor([t["prompt"] + raw[:-1]]))["logits"][0].float()
+    cand = list(raw)
+    while len(cand) > 1 and cand[-1] == 50257 and cand[-2] == 50257:
+        cand = cand[:-1]
+    scores = []
+    for j in range(len(cand)):
+        row = lg[P - 1 + j].clone()
         row[mg.SUPPRESS] = -float("inf")
-        if i == 0:
+        if j == 0:
             row[[220, 50257]] = -float("inf")
-        r = timestamp_rules(row, raw[:i], i == 0, max_initial=50, apply_mass=False)
-        ts, tx = r[50364:], r[:50364]
-        if torch.isfinite(ts).any() and torch.isfinite(tx).any():
-            best = min(best, abs(float(torch.logsumexp(ts, -1) - tx.max())))
-    return best
+        scores.append(greedy_ref.timestamp_rules(row, raw[:j], j == 0, max_initial=50))
+    return greedy_ref.avg_logprob(scores, cand)

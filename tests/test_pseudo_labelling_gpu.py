@@ -64,7 +64,9 @@ def test_pseudo_labelling_entry_point(tmp_path):
         w, sr = read_audio(p)
         chunks += [(p, s, e, c) for s, e, c in pl.chunk_audio(w, sr, 5)]
     assert len(chunks) == 3 + 1 + 2
-    m2 = WhisperForConditionalGeneration.from_pretrained(str(ck), torch_dtype=torch.bfloat16)
+    # --compute_type default -> the fp16 model (CTranslate2's CUDA default for a float16 checkpoint)
+    m2 = WhisperForConditionalGeneration.from_pretrained(str(ck), torch_dtype=torch.float16)
+    assert m2.compute == "fp16"
     tr = pl.ChunkTranscriber(m2, "zh", 24)
     dec = pl.load_text_decoder(pl.parse_args(["--byte_level_text_tokenizer", "True"]))
     want = {}
