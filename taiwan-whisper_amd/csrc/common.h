@@ -45,8 +45,15 @@ __device__ __forceinline__ float e2f(bf16 x) {
 }
 template <bool H>
 __device__ __forceinline__ bf16 f2e(float x) {
-  if constexpr (H) return __builtin_bit_cast(bf16, (_Float16)x);
-  else return (bf16)x;
+  if constexpr (H) {
+    // x is materialised as an fp32 value first: without this the backend folds fptrunc(fma(a, b, c)) into
+    // v_fma_mixlo_f16, which rounds the exact a*b+c to fp16 ONCE -- the reference (an fp32 GEMM epilogue, then
+    // the cast) rounds twice, and the two differ on ~2e-5 of the outputs (tests/test_fp16_gpu.py)
+    asm("" : "+v"(x));
+    return __builtin_bit_cast(bf16, (_Float16)x);
+  } else {
+    return (bf16)x;
+  }
 }
 template <bool H>
 __device__ __forceinline__ float rnd(float x) { return e2f<H>(f2e<H>(x)); }

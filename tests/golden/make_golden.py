@@ -399,6 +399,11 @@ CFG_CASES = {
     # frozen shared encoder, a <|startofprev|> prompt (A7 teacher-input quirk at full size)
     "c3": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=1, freeze_encoder=True,
                freeze_embed_positions=True, label_seed=43, secs=[30.0], prompt=True),
+    # c3 at B = 10: encoder rows 15 000 and decoder rows 4 470 (>= 4096), so the projections take the production
+    # route of the B = 64 step (tw_gemm_backend: hipBLASLt for the plain bias projections)
+    "c3b10": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=10, freeze_encoder=True,
+                  freeze_embed_positions=True, label_seed=45, secs=[30.0, 27.5, 12.0, 30.0, 8.0, 19.0, 30.0, 24.0,
+                                                                    30.0, 15.5], prompt=True),
 }
 
 
@@ -512,7 +517,7 @@ def main():
     for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
-                     ("cfg_c3", lambda o: gen_cfg("c3", o))):
+                     ("cfg_c3", lambda o: gen_cfg("c3", o)), ("cfg_c3b10", lambda o: gen_cfg("c3b10", o))):
         if only and name not in only:
             continue
         out = {}

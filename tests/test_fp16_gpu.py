@@ -100,7 +100,9 @@ def test_gemm_f16_gelu_residual_clamp():
     X = res.clone()
     ops.gemm(A, W, X, M, N, K, lda=K, ldb=K, ldc=N, bias=b, res=X, ldr=N, flags=ops.GEMM_ROUND | ops.GEMM_CLAMP16)
     want = (P.float() + res.float()).half().float().clamp(-64504.0, 64504.0).half()
-    assert torch.equal(X, want)
+    bad = (X.float() != want.float()).nonzero()
+    assert bad.shape[0] == 0, (bad.shape[0], bad[:6].tolist(), [(float(X[i, j]), float(want[i, j]), float(P[i, j]),
+                                                                float(res[i, j])) for i, j in bad[:6].tolist()])
     assert torch.isfinite(X.float()).all() and (X.float()[:8] > 60000).all() and (X.float()[:16].abs() <= 64512).all()
 
 
@@ -233,7 +235,7 @@ def test_fp16_timestamps_longform_fallback_vs_hf():
     from test_decode_gpu import _feats
     feats = _feats()[:2]
     gen = m.generate(feats, return_timestamps=True, language="zh", task="transcribe", max_new_tokens=48).cpu()
-    np.testing.assert_array_equal(gen.numpy(), h["f16_ts_short_ids"])
+    _equal_or_fp32_near_tie(gen.numpy(), h["f16_ts_short_ids"], feats, [50258, 50260, 50359], mg.SUPPRESS)
     lf = torch.from_numpy(mg.longform_features())
     kw = dict(attention_mask=torch.ones(1, lf.shape[-1], dtype=torch.long), return_timestamps=True, language="zh",
               task="transcribe")
@@ -252,6 +254,36 @@ def test_fp16_timestamps_longform_fallback_vs_hf():
     np.testing.assert_allclose([t["avg_logprob"] for t in trace], h["f16_fb_avg_logprobs"], rtol=0, atol=2e-2)
     for t in trace:
         assert abs(t["avg_logprob"] - _oracle_avg(lf, t)) <= 5e-3
+
+
+def _equal_or_fp32_near_tie(got, want, feats, prompt, suppress):
+    """Timestamp ids equal HF fp16's, or each row leaves HF's sequence at a position where the two candidate
+    tokens are a near-tie BY THE fp32 REFERENCE: the fp32 oracle (CPU, pinned to HF fp32) teacher-forced along
+    HF's prefix puts their processed logits within 2 fp16 ulps of each other (below fp16's own resolution there:
+    measured, row 0 token 14 of the short-form fixture: fp32 margin 6.8e-4, both fp16 logits 11.0625 -- an exact
+    fp16 tie that HF's CPU kernels broke by lowest id).  After the divergence the row is not compared."""
+    from oracle import greedy_ref
+    from oracle.weights import CONFIGS, make_weights
+    from oracle.whisper_ref import Ref, to_torch
+    ref32 = Ref(CONFIGS["micro"], to_torch(make_weights(CONFIGS["micro"], 1, lin_std=0.2)))
+    for b in range(want.shape[0]):
+        d = np.nonzero(got[b] != want[b])[0]
+        if len(d) == 0:
+            continue
+        j = int(d[0])
+        prefix = want[b, :j].tolist()
+        with torch.no_grad():
+            lg = ref32.forward(feats[b:b + 1].float(), torch.tensor([list(prompt) + prefix]))["logits"][0].float()
+        row = lg[len(prompt) - 1 + j].clone()
+        row[suppress] = -float("inf")
+        if j == 0:
+            row[[220, 50257]] = -float("inf")
+        r = greedy_ref.timestamp_rules(row, prefix, j == 0, max_initial=50)
+        a, c = int(want[b, j]), int(got[b, j])
+        ulp = 2.0 ** (np.floor(np.log2(max(abs(float(r[a])), 2.0 ** -14))) - 10)
+        margin = abs(float(r[a] - r[c]))
+        print(f"row {b} leaves HF fp16 at token {j}: {a} vs {c}, fp32 margin {margin:.2e} ({margin / ulp:.2f} fp16 ulps)")
+        assert margin <= 2 * ulp, (b, j, a, c, margin, ulp)
 
 
 def _oracle_avg(lf, t):
