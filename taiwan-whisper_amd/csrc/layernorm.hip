@@ -99,25 +99,45 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                           int rows, int D, float eps, const bf16* __restrict__ r = nullptr,
                                                           bf16* x_out = nullptr) {
+  // gamma / beta staged once per block in LDS (8 rows share them), so the output pass has no global loads
+  __shared__ f32x4 sw[NCH * 64], sb[NCH * 64];
   const int lane = lane_id(), hl = lane & 31;
   const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   const bool ok = row < rows;
-  const int64_t base = (int64_t)(ok ? row : 0) * D;
-  float v[NCH][8];
+  // a tail half-wave reads the last row (in range) unconditionally and stores nothing: every load of the
+  // row is issued before the first wait (no per-chunk branch + vmcnt(0) round trip)
+  const int64_t base = (int64_t)(ok ? row : rows - 1) * D;
+  constexpr int KS = (NCH * 64 + 255) / 256;
+  int ix[KS];
+  f32x4 gw[KS], gb[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {  // gamma / beta loads first: waiting on them does not wait on the rows
+    ix[k] = min((int)threadIdx.x + k * 256, NCH * 64 - 1);
+    gw[k] = ((const f32x4*)w)[ix[k]];
+    gb[k] = ((const f32x4*)b)[ix[k]];
+  }
+  bf16x8 t[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) t[c] = *(const bf16x8*)(x + base + (c * 32 + hl) * 8);
+  if constexpr (ADD) {
+    bf16x8 u[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) u[c] = *(const bf16x8*)(r + base + (c * 32 + hl) * 8);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[c][q] = f2e<H>(e2f<H>(t[c][q]) + e2f<H>(u[c][q]));
+  }
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {  // stage (the loads were issued first; a clamped index rewrites the same value)
+    sw[ix[k]] = gw[k];
+    sb[ix[k]] = gb[k];
+  }
   float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int e = (c * 32 + hl) * 8;
-    bf16x8 t = ok ? *(const bf16x8*)(x + base + e) : bf16x8{};
-    if constexpr (ADD) {
-      const bf16x8 u = ok ? *(const bf16x8*)(r + base + e) : bf16x8{};
+  for (int c = 0; c < NCH; ++c)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) t[q] = f2e<H>(e2f<H>(t[q]) + e2f<H>(u[q]));
-      if (ok) *(bf16x8*)(x_out + base + e) = t;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { v[c][q] = e2f<H>(t[q]); s += v[c][q]; }
-  }
+    for (int q = 0; q < 8; ++q) s += e2f<H>(t[c][q]);
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   const float mean = s / D;
@@ -125,10 +145,11 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) { const float d = v[c][q] - mean; ss += d * d; }
+    for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[c][q]) - mean; ss += d * d; }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
   const float rstd = rsqrtf(ss / D + eps);
+  __syncthreads();
   if (!ok) return;
   if (hl == 0) {
     if (mean_out) mean_out[row] = mean;
@@ -137,13 +158,13 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int e = (c * 32 + hl) * 8;
-    const f32x4 w0 = *(const f32x4*)(w + e), w1 = *(const f32x4*)(w + e + 4);
-    const f32x4 b0 = *(const f32x4*)(b + e), b1 = *(const f32x4*)(b + e + 4);
+    if constexpr (ADD) *(bf16x8*)(x_out + base + e) = t[c];
+    const f32x4 w0 = sw[e / 4], w1 = sw[e / 4 + 1], b0 = sb[e / 4], b1 = sb[e / 4 + 1];
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      o[q] = f2e<H>((v[c][q] - mean) * rstd * w0[q] + b0[q]);
-      o[q + 4] = f2e<H>((v[c][q + 4] - mean) * rstd * w1[q] + b1[q]);
+      o[q] = f2e<H>((e2f<H>(t[c][q]) - mean) * rstd * w0[q] + b0[q]);
+      o[q + 4] = f2e<H>((e2f<H>(t[c][q + 4]) - mean) * rstd * w1[q] + b1[q]);
     }
     *(bf16x8*)(y + base + e) = o;
   }
