@@ -388,6 +388,7 @@ def main():
 
     for i in range(args.warmup):
         m = step(i)
+    trainer.flush()              # the warmup's last update (deferred under DP) stays outside the timed region
     torch.cuda.synchronize()
     if pg is not None:
         torch.distributed.barrier()
@@ -397,6 +398,7 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             m = step(i)
+        trainer.flush()          # ... and the last timed step's update inside it: exactly K updates timed
         torch.cuda.synchronize()
         if pg is not None:
             torch.distributed.barrier()

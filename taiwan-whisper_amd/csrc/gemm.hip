@@ -165,6 +165,23 @@ __device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_
   }
 }
 
+// Epilogue of fragment rows MI0 .. MI1-1 of finished tile `ti` of this workgroup, then those accumulators
+// are zeroed for the next tile.  Debug flags: 4096 skips the stores, 1 << 20 stores every tile to tile 0.
+template <bool H, int KIND, int MI0, int MI1>
+__device__ __forceinline__ void pp_epi_part(const GemmP& p, f32x4 (&acc)[8][4], int ti, int wm, int wn, int lane,
+                                            const bf16* braw) {
+  if (!(p.flags & 4096) || acc[MI0][0][0] != acc[MI0][0][0]) {
+    int m0, n0, bz;
+    pp_tile(p, ti, m0, n0, bz);
+    if (p.flags & (1 << 20)) { m0 = 0; n0 = 0; }
+    epilogue_k<H, 256, 256, 2, 4, KIND, MI0, MI1, true>(p, acc, m0, n0, wm, wn, lane, bz, braw);
+  }
+#pragma unroll
+  for (int i = MI0; i < MI1; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 // Persistent form: gridDim.x (a multiple of 8, <= CUs) workgroups; workgroup b takes the tiles
 // of virtual block ids b, b + G, b + 2G, ... (G = gridDim.x), each mapped through the same
 // XCD-aware bijective remap as a one-tile-per-block launch, so an XCD keeps walking its own
@@ -176,9 +193,11 @@ __device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_
 // prio 1 around each MFMA phase; 1 = the same with static prio 1 for the trailing wave row
 // (waves 4-7), no flips; 2 = diagnostic: every MFMA phase issued twice (wrong results; measures
 // the fixed per-phase cost); 4 = two 32-MFMA phases per K-tile (default: +4-8 % main loop)
-template <bool H, int PRIO>
+template <bool H, int PRIO, int KIND = -1>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_REGION];
+  // + 2 x 1 KiB: the bias slice of the current tile (by tile parity), for the fast epilogue (one array:
+  // a second __shared__ object can make the compiler drain vmcnt before LDS reads)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_REGION + 2048];
   const int lane = lane_id();
   const int wave = wave_id_uniform();
   const int wm = wave >> 2, wn = wave & 3;
@@ -187,6 +206,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const int my_tiles = ((int)blockIdx.x < p.tiles_total) ? (p.tiles_total - (int)blockIdx.x + G - 1) / G : 0;
   const int total = my_tiles * nke;                       // K-tiles this workgroup consumes
 
+  int si = 0;                                // current tile of this workgroup
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -289,10 +309,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const bf16 *cpa, *cpb;                     // current tile (see tile_info)
   int cr, cc, ck;
   tile_info(0, cpa, cpb, cr, cc, ck);
-  int kt = 0, ti = 0;
+  int kt = 0;
   stage(cpa, cpb, cr, cc, ck, 0, 0, 0); stage(cpa, cpb, cr, cc, ck, 0, 0, 1);
   stage(cpa, cpb, cr, cc, ck, 0, 0, 2); stage(cpa, cpb, cr, cc, ck, 0, 0, 3);
-  if constexpr (PRIO >= 4) {                 // K-tile 1 without its A-half 1 (staged in the first phase)
+  if constexpr (PRIO >= 3) {                 // K-tile 1 without its A-half 1 (staged in the first phase)
     stage(cpa, cpb, cr, cc, ck, 1, 1, 0); stage(cpa, cpb, cr, cc, ck, 1, 1, 2); stage(cpa, cpb, cr, cc, ck, 1, 1, 3);
   } else {
     stage(cpa, cpb, cr, cc, ck, 1, 1, 0); stage(cpa, cpb, cr, cc, ck, 1, 1, 3); stage(cpa, cpb, cr, cc, ck, 1, 1, 1);
@@ -304,14 +324,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 
   for (int g = 0; g < total; g += 2) {
     // K-tiles g, g+1 = (cur, kt), (cur, kt+1); g+2, g+3 = (nxt, k2), (nxt, k2+1)
-    const bool last = kt + 2 >= nke;
+    const bool last = kt + 2 >= nke;                            // this pair ends the tile
     const bf16 *npa = cpa, *npb = cpb;
     int nr = cr, nc = cc, nkl = ck, k2 = kt + 2;
     if (last) {
-      tile_info(ti + 1, npa, npb, nr, nc, nkl);
+      tile_info(si + 1, npa, npb, nr, nc, nkl);
       k2 = 0;
     }
-    if constexpr (PRIO >= 4) {
+    if constexpr (PRIO >= 3) {
       // Two phases per K-tile (A-half 0, then A-half 1, each against both B-quarters): the load
       // segment before phase X reads A0, B0, B1 and stages A1 of the next K-tile; the one before
       // phase Y reads A1 and stages A0, B0, B1 of the K-tile two ahead (their last readers, the
@@ -321,16 +341,27 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       // readers' segments.
       if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // PRIO 7: diagnostic, no waits
       rdA(0, 0); rdB2(0); stg(cpa, cpb, cr, cc, ck, kt + 1, 1, 1);
+      // a tile's first K-tile pair: wave 0 stages its 256 bias words (LDS-DMA, no registers).  The next-but-one
+      // counted wait of wave 0 covers it and a barrier follows, long before the tile's epilogue reads it;
+      // the extra DMA only makes wave 0's counted waits stricter.
+      if (kt == 0 && (p.flags & F_BIAS) && wave == 0) {
+        int m0, n0, bz;
+        if (pp_tile(p, si, m0, n0, bz)) {
+          const int c = n0 + lane * 8;                          // 8 words per lane, lanes 0..31
+          const uint32_t o = (lane < 32 && c < p.N) ? (uint32_t)(c * 2) : TW_OOB;
+          buf_load_lds16(make_rsrc(p.bias), smem + 8 * PP_REGION + (si & 1) * 1024, o);
+        }
+      }
       mma2(0);
       if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      if constexpr (PRIO == 4) rdA(0, 1);      // PRIO 5: diagnostic, A-half 1 not read (LDS-read cost)
+      if constexpr (PRIO == 4 || PRIO == 3) rdA(0, 1);      // PRIO 5: diagnostic, A-half 1 not read (LDS-read cost)
       stg(npa, npb, nr, nc, nkl, k2, 0, 0); stg(npa, npb, nr, nc, nkl, k2, 0, 2); stg(npa, npb, nr, nc, nkl, k2, 0, 3);
       mma2(1);
       if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // PRIO 7: diagnostic, no waits
       rdA(1, 0); rdB2(1); stg(npa, npb, nr, nc, nkl, k2, 0, 1);
       mma2(0);
       if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      if constexpr (PRIO == 4) rdA(1, 1);
+      if constexpr (PRIO == 4 || PRIO == 3) rdA(1, 1);
       stg(npa, npb, nr, nc, nkl, k2 + 1, 1, 0); stg(npa, npb, nr, nc, nkl, k2 + 1, 1, 2); stg(npa, npb, nr, nc, nkl, k2 + 1, 1, 3);
       mma2(1);
     } else {
@@ -348,17 +379,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");            mma(1, 0);
     }
     if (last) {                                                 // tile finished
-      if (!(p.flags & 4096) || acc[0][0][0] != acc[0][0][0])    // 4096: diagnostic, skip epilogue
-      {
-        int m0, n0, bz;
-        pp_tile(p, ti, m0, n0, bz);
-        epilogue<H, 256, 256, 2, 4>(p, acc, m0, n0, wm, wn, lane, bz);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ++ti;
+      pp_epi_part<H, KIND, 0, 8>(p, acc, si, wm, wn, lane, (const bf16*)(smem + 8 * PP_REGION + (si & 1) * 1024));
+      ++si;
     }
     cpa = npa; cpb = npb; cr = nr; cc = nc; ck = nkl;
     kt = k2;
@@ -735,6 +757,21 @@ int pick_epilogue(const GemmP& p, int batch) {
   return EPI_GENERIC;
 }
 
+// the production variants are specialised on the epilogue kind (one fast epilogue + the generic one for
+// ragged tiles per kernel: the split epilogue's three inlined parts stay within the register budget)
+template <bool H, int PRIO>
+void launch_pp_kind(const GemmP& p, int grid, hipStream_t stream) {
+  switch (p.epi) {
+    case EPI_STORE_BF16: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_STORE_BF16>), dim3(grid), dim3(512), 0, stream, p); break;
+    case EPI_STORE_F32: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_STORE_F32>), dim3(grid), dim3(512), 0, stream, p); break;
+    case EPI_GELU: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_GELU>), dim3(grid), dim3(512), 0, stream, p); break;
+    case EPI_GELU_AUX: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_GELU_AUX>), dim3(grid), dim3(512), 0, stream, p); break;
+    case EPI_RES_BF16: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_RES_BF16>), dim3(grid), dim3(512), 0, stream, p); break;
+    case EPI_RES_F32: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_RES_F32>), dim3(grid), dim3(512), 0, stream, p); break;
+    default: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_GENERIC>), dim3(grid), dim3(512), 0, stream, p); break;
+  }
+}
+
 template <bool H>
 void launch_pp(GemmP p, int batch, hipStream_t stream) {
   static const int cus = [] {
@@ -754,14 +791,18 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
     const char* e = getenv("TW_PP_VARIANT");   // A/B runs of whole steps only (bench.py)
     return e ? atoi(e) : -1;
   }();
+  // (the round-2 diagnostic variants PRIO 0/1/2/5/6/7 stay in the source but are no longer instantiated:
+  // each is a full copy of the kernel; TW_PP_DIAG_VARIANTS=1 at build time brings them back)
   switch (env_variant >= 0 ? env_variant : (p.flags >> 15) & 7) {
+#ifdef TW_PP_DIAG_VARIANTS
     case 1: hipLaunchKernelGGL((gemm_pp_kernel<H, 0>), dim3(grid), dim3(512), 0, stream, p); break;
     case 2: hipLaunchKernelGGL((gemm_pp_kernel<H, 2>), dim3(grid), dim3(512), 0, stream, p); break;
     case 3: hipLaunchKernelGGL((gemm_pp_kernel<H, 1>), dim3(grid), dim3(512), 0, stream, p); break;
     case 5: hipLaunchKernelGGL((gemm_pp_kernel<H, 5>), dim3(grid), dim3(512), 0, stream, p); break;
     case 6: hipLaunchKernelGGL((gemm_pp_kernel<H, 6>), dim3(grid), dim3(512), 0, stream, p); break;
     case 7: hipLaunchKernelGGL((gemm_pp_kernel<H, 7>), dim3(grid), dim3(512), 0, stream, p); break;
-    default: hipLaunchKernelGGL((gemm_pp_kernel<H, 4>), dim3(grid), dim3(512), 0, stream, p); break;
+#endif
+    default: launch_pp_kind<H, 4>(p, grid, stream); break;
   }
 }
 

@@ -136,14 +136,18 @@ __device__ __forceinline__ void tile_coords(int tid, const GemmP& p, int& mt, in
 
 // Generic epilogue (any flag combination, ragged edges): lane holds C[m][n..n+3] of each 16x16
 // fragment (swapped-operand MFMA layout).
-template <bool H, int BM, int BN, int WM, int WN>
+// MI0 .. MI1 (MI1 < 0: all): the fragment rows written (the persistent kernel splits a tile's epilogue
+// over several load segments).
+// RAGGED: only ever called for tiles past an edge (no full-tile vector path compiled in).
+template <bool H, int BM, int BN, int WM, int WN, int MI0 = 0, int MI1 = -1, bool RAGGED = false>
 __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                          int n0, int wm, int wn, int lane, int bz) {
-  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int FN = BN / WN / 16;
+  constexpr int FM = MI1 < 0 ? BM / WM / 16 : MI1;
   const int g = lane >> 4, li = lane & 15;
   const int flags = p.flags;
   char* C = (char*)p.C;
-  const bool full_tile = (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 3) == 0) &&
+  const bool full_tile = !RAGGED && (m0 + BM <= p.M) && (n0 + BN <= p.N) && ((p.ldc & 3) == 0) &&
                          (!(flags & F_RES) || ((p.ldr & 3) == 0 && p.res_mod == 0)) &&
                          (!(flags & (F_AUX_OUT | F_DGELU)) || (p.ldaux & 3) == 0);
   if (full_tile) {
@@ -162,7 +166,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
       }
     }
 #pragma unroll
-    for (int mi = 0; mi < FM; ++mi) {
+    for (int mi = MI0; mi < FM; ++mi) {
       const int m = m0 + wm * (BM / WM) + mi * 16 + li;
       const int nb = n0 + wn * (BN / WN) + 4 * g;
       float ex[FN][4];     // residual / old-C / aux operand, loaded up front
@@ -224,7 +228,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
     return;
   }
 #pragma unroll
-  for (int mi = 0; mi < FM; ++mi) {
+  for (int mi = MI0; mi < FM; ++mi) {
     const int m = m0 + wm * (BM / WM) + mi * 16 + li;
     if (m >= p.M) continue;
 #pragma unroll
@@ -335,45 +339,78 @@ __device__ __forceinline__ void u4_to_pair(u32x4 r, float (&x)[4], float (&y)[4]
   y[0] = lo_e<H>(s0[1]); y[1] = hi_e<H>(s0[1]); y[2] = lo_e<H>(s1[1]); y[3] = hi_e<H>(s1[1]);
 }
 
-template <bool H, int BM, int BN, int WM, int WN, int KIND>
+// PB: the tile's bias was staged in LDS (`braw` = its first column, see gemm_pp_kernel) -- a global load
+// inside the epilogue would wait for every LDS-DMA still in flight (loads retire in order).  Without bias,
+// -0.0 is added (the neutral element: x + -0.0 == x for every x, signed zeros included).
+template <bool H, int BM, int BN, int WM, int WN, int KIND, int MI0 = 0, int MI1 = -1, bool PB = false>
 __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                              int n0, int wm, int wn, int lane, int bz) {
-  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+                                              int n0, int wm, int wn, int lane, int bz,
+                                              const bf16* braw = nullptr) {
+  constexpr int FN = BN / WN / 16;
+  constexpr int FM = MI1 < 0 ? BM / WM / 16 : MI1;
   static_assert(FN % 2 == 0, "fragment pairs");
   const int g = lane >> 4, li = lane & 15;
   const int cw = n0 + wn * (BN / WN);                 // wave's first column
   const int sw = (g & 1) * 16 + (g >> 1) * 8;        // this lane's column in a swapped pair
   const bool rd = p.flags & F_ROUND;
   float bv[FN][4];
+  if constexpr (PB) {
+    const bool hb = p.flags & F_BIAS;
 #pragma unroll
-  for (int ni = 0; ni < FN; ++ni) {
-    if (p.flags & F_BIAS) {
-      const bf16x4 t = *(const bf16x4*)(p.bias + cw + ni * 16 + 4 * g);
+    for (int ni = 0; ni < FN; ++ni)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[ni][r] = e2f<H>(t[r]);
-    } else {
+      for (int r = 0; r < 4; ++r) bv[ni][r] = -0.f;
+    if (hb) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
+      for (int ni = 0; ni < FN; ++ni) {
+        const bf16x4 t = *(const bf16x4*)(braw + wn * (BN / WN) + ni * 16 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[ni][r] = e2f<H>(t[r]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int ni = 0; ni < FN; ++ni) {
+      if (p.flags & F_BIAS) {
+        const bf16x4 t = *(const bf16x4*)(p.bias + cw + ni * 16 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[ni][r] = e2f<H>(t[r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[ni][r] = 0.f;
+      }
     }
   }
+  // Residual operands are loaded a batch of row blocks at a time (2: 16 / 32 VGPRs within the budget),
+  // before any store of those rows (in-place updates): one memory round trip per batch instead of one per
+  // row block (each load waits for everything issued before it, LDS-DMA included).
+  constexpr int RB = KIND == EPI_RES_BF16 ? 2 : (KIND == EPI_RES_F32 ? 2 : 1);
 #pragma unroll
-  for (int mi = 0; mi < FM; ++mi) {
-    const int64_t m = m0 + wm * (BM / WM) + mi * 16 + li;
-    // residual operand of the whole row block, loaded before any store of it
-    u32x4 rb[FN / 2];
-    f32x4 rf[FN];
+  for (int mb = MI0; mb < FM; mb += RB) {
+  u32x4 rball[KIND == EPI_RES_BF16 ? RB : 1][FN / 2];
+  f32x4 rfall[KIND == EPI_RES_F32 ? RB : 1][FN];
+#pragma unroll
+  for (int q = 0; q < RB && mb + q < FM; ++q) {
+    const int64_t m = m0 + wm * (BM / WM) + (mb + q) * 16 + li;
     if constexpr (KIND == EPI_RES_BF16) {
       const bf16* rrow = (const bf16*)p.res + bz * p.sR + m * p.ldr + cw;
 #pragma unroll
       for (int np = 0; np < FN / 2; ++np)
-        rb[np] = *(const u32x4*)(rrow + np * 32 + sw);
+        rball[q][np] = *(const u32x4*)(rrow + np * 32 + sw);
     }
     if constexpr (KIND == EPI_RES_F32) {
       const float* rrow = (const float*)p.res + bz * p.sR + m * p.ldr + cw;
 #pragma unroll
       for (int ni = 0; ni < FN; ++ni)
-        rf[ni] = *(const f32x4*)(rrow + ni * 16 + 4 * g);
+        rfall[q][ni] = *(const f32x4*)(rrow + ni * 16 + 4 * g);
     }
+  }
+#pragma unroll
+  for (int q = 0; q < RB && mb + q < FM; ++q) {
+    const int mi = mb + q;
+    const int64_t m = m0 + wm * (BM / WM) + mi * 16 + li;
+    const auto& rb = rball[KIND == EPI_RES_BF16 ? q : 0];
+    const auto& rf = rfall[KIND == EPI_RES_F32 ? q : 0];
 #pragma unroll
     for (int np = 0; np < FN / 2; ++np) {
       float v[2][4];
@@ -383,9 +420,7 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
         for (int r = 0; r < 4; ++r) v[h][r] = p.alpha * acc[mi][2 * np + h][r] + bv[2 * np + h][r];
       if constexpr (KIND == EPI_STORE_BF16) {
         bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
-        const u32x4 o = pair_to_u4<H>(v[0], v[1]);
-        // (1 << 21): diagnostic, compute but do not store (timing only)
-        if (!(p.flags & (1 << 21)) || o[0] == 0x7fc17fc1u) *(u32x4*)(crow + np * 32 + sw) = o;
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
       } else if constexpr (KIND == EPI_STORE_F32) {
         float* crow = (float*)p.C + bz * p.sC + m * p.ldc + cw;
 #pragma unroll
@@ -448,20 +483,38 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
       }
     }
   }
+  }
 }
 
-template <bool H, int BM, int BN, int WM, int WN>
+template <bool H, int BM, int BN, int WM, int WN, int MI0 = 0, int MI1 = -1>
 __device__ __forceinline__ void epilogue(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                          int n0, int wm, int wn, int lane, int bz) {
   const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
   const int k = full ? p.epi : EPI_GENERIC;
-  if (k == EPI_STORE_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_STORE_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_F32>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_GELU) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_GELU_AUX) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU_AUX>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_RES_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_RES_BF16>(p, acc, m0, n0, wm, wn, lane, bz);
-  else if (k == EPI_RES_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_RES_F32>(p, acc, m0, n0, wm, wn, lane, bz);
-  else epilogue_generic<H, BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
+  if (k == EPI_STORE_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_BF16, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_STORE_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_F32, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_GELU) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_GELU_AUX) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU_AUX, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_RES_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_RES_BF16, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  else if (k == EPI_RES_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_RES_F32, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  else epilogue_generic<H, BM, BN, WM, WN, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+}
+
+// The same with the kind fixed at compile time (KIND < 0: the runtime dispatch above); ragged tiles
+// take the generic form.
+template <bool H, int BM, int BN, int WM, int WN, int KIND, int MI0 = 0, int MI1 = -1, bool PB = false>
+__device__ __forceinline__ void epilogue_k(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                           int n0, int wm, int wn, int lane, int bz, const bf16* braw = nullptr) {
+  if constexpr (KIND < 0) {
+    epilogue<H, BM, BN, WM, WN, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  } else if constexpr (KIND == EPI_GENERIC) {
+    epilogue_generic<H, BM, BN, WM, WN, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+  } else {
+    if ((m0 + BM <= p.M) && (n0 + BN <= p.N))
+      epilogue_fast<H, BM, BN, WM, WN, KIND, MI0, MI1, PB>(p, acc, m0, n0, wm, wn, lane, bz, braw);
+    else
+      epilogue_generic<H, BM, BN, WM, WN, MI0, MI1, true>(p, acc, m0, n0, wm, wn, lane, bz);
+  }
 }
 
 __device__ __forceinline__ bool pp_tile(const GemmP& p, int i, int& m0, int& n0, int& bz) {

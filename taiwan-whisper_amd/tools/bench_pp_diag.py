@@ -8,15 +8,16 @@ import torch
 
 from tw import ops
 
-VARIANTS = (("persist", 0), ("persist-noepi", 4096), ("1tile", 8192), ("1tile-noepi", 8192 | 4096))
+VARIANTS = (("pp", 0), ("noepi", 4096))
 
 
 def main(rounds=5):
-    for M, N, K in ((96000, 5120, 1280), (96000, 1280, 5120), (4096, 4096, 4096), (8192, 8192, 8192)):
+    for M, N, K in ((96000, 5120, 1280), (28608, 3840, 1280), (28608, 51904, 1280), (96000, 1280, 5120)):
         A = torch.randn(M, K, device="cuda").bfloat16()
         B = torch.randn(N, K, device="cuda").bfloat16()
         C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-        run = lambda f: ops.gemm(A, B, C, M, N, K, lda=K, ldb=K, ldc=N, flags=ops.GEMM_ROUND | ops.GEMM_TILE256PP | f)
+        bias = torch.randn(N, device="cuda").bfloat16()
+        run = lambda f: ops.gemm(A, B, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bias, flags=ops.GEMM_ROUND | ops.GEMM_BIAS | ops.GEMM_TILE256PP | f)
         for _, f in VARIANTS:
             run(f); run(f)
         t = {v: [] for v, _ in VARIANTS}
@@ -30,10 +31,10 @@ def main(rounds=5):
                 torch.cuda.synchronize()
                 t[v].append(e0.elapsed_time(e1) / 3)
         fl = 2.0 * M * N * K
-        line = f"M={M:6d} N={N:5d} K={K:5d} "
+        line = f"M={M:6d} N={N:5d} K={K:5d}\n"
         for v, _ in VARIANTS:
             ms = sorted(t[v])[len(t[v]) // 2]
-            line += f"{v}: {ms*1e3:7.1f}us {fl/ms/1e9:6.1f}TF  "
+            line += f"   {v:14s}: {ms*1e3:7.1f}us {fl/ms/1e9:6.1f}TF\n"
         print(line, flush=True)
 
 

@@ -78,7 +78,8 @@ class DistillationTrainer:
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, warmup_steps: int = 0,
                  lr_scheduler_type: str = "constant_with_warmup", max_steps: int = 0,
                  gradient_accumulation_steps: int = 1, freeze_encoder: bool = True, freeze_decoder: bool = False,
-                 freeze_embed_positions: bool = True, process_group=None, dp_bucket_mb: int = 64):
+                 freeze_embed_positions: bool = True, process_group=None, dp_bucket_mb: int = 64,
+                 overlap_update: Optional[bool] = None):
         if student.compute != teacher.compute:
             raise ValueError(f"student computes in {student.compute}, teacher in {teacher.compute}: the reference "
                              "runs both under one mixed_precision setting")
@@ -96,6 +97,16 @@ class DistillationTrainer:
         # exact and commutes with every rounding of the backward, so it is folded into the loss gradient
         # (no extra pass); otherwise each slice is scaled right before its all-reduce, as DDP does.
         self.fold_world = self.world & (self.world - 1) == 0
+        # Deferred update (DP, frozen encoder): the gradient exchange of the sync micro-step is launched at
+        # its end, but the wait + clip + AdamW are queued only after the NEXT step's encoder forward, which
+        # reads no trainable weight.  The exchange of the last-finished gradients (the tied embedding,
+        # 265 MB at c3, final only after the embedding backward) then runs beside that encoder instead of
+        # stalling the stream.  Same kernels on the same data in the same order per buffer: bit-identical.
+        # Any reader of the weights or optimizer state (eval, state dicts, save) calls flush() first.
+        self.overlap_update = (self.world > 1 and freeze_encoder) if overlap_update is None else bool(overlap_update)
+        if self.overlap_update and not freeze_encoder:
+            raise ValueError("overlap_update needs a frozen encoder: the next forward must read no trainable weight")
+        self._update = None      # (lr, t) of a launched, not yet applied update
         set_trainable_like_reference(student, freeze_encoder, freeze_decoder, freeze_embed_positions)
         self.train_encoder = not freeze_encoder
         self.freeze_encoder, self.freeze_decoder = freeze_encoder, freeze_decoder
@@ -159,6 +170,9 @@ class DistillationTrainer:
         ids = batch["decoder_input_ids"].to(s.device).contiguous()
         labels = batch["labels"].to(s.device).contiguous()
         B, Td = ids.shape
+        enc_tape = [] if self.train_encoder else None
+        enc16 = s.encode(conv_in, tape=enc_tape)
+        self.flush()             # the previous update (its exchange ran beside the encoder above)
         if self.micro == 0:
             s.grad.zero_()
         # DP: on the micro-step that syncs, each layer's gradient slice is all-reduced as soon as
@@ -166,8 +180,6 @@ class DistillationTrainer:
         self._pending, self._reduced = [], []
         sync = self.micro + 1 == self.accum or end_of_dataloader
         self.bw.on_ready = self._grad_ready if (self.world > 1 and sync) else None
-        enc_tape = [] if self.train_encoder else None
-        enc16 = s.encode(conv_in, tape=enc_tape)
         Tk = enc16.shape[0] // B
         tape = []
         hs = s.decode(ids, enc16, Tk, tape=tape)
@@ -194,6 +206,7 @@ class DistillationTrainer:
 
     def eval_step(self, batch):
         """run_distillation.py:1554-1578: T = 1, no grad."""
+        self.flush()
         s = self.s
         conv_in = self._conv_input(batch)
         ids = batch["decoder_input_ids"].to(s.device).contiguous()
@@ -224,11 +237,11 @@ class DistillationTrainer:
         if r is not None:
             self._launch(*r)
 
-    def all_reduce_grads(self):
-        """DDP mean over ranks: bucketed SUM all-reduce of the flat fp32 gradient over RCCL, each rank's
-        gradient scaled by 1/world first (folded into the loss gradient for power-of-two worlds).  Ranges whose exchange already
-        started during the backward (per finished layer) are skipped; the rest (embeddings, final
-        LayerNorm, ...) is launched now, then everything is waited for."""
+    def launch_grad_exchange(self):
+        """Launch the part of the DDP-mean exchange not yet started: ranges whose exchange began during
+        the backward (per finished layer) are skipped; the rest (embeddings, final LayerNorm, ...) is
+        launched now.  Bucketed async SUM all-reduce of the flat fp32 gradient over RCCL, each rank's
+        gradient scaled by 1/world first (folded into the loss gradient for power-of-two worlds)."""
         if self.world == 1:
             return
         done = sorted(getattr(self, "_reduced", []))
@@ -239,28 +252,56 @@ class DistillationTrainer:
             if lo > pos:
                 self._launch(pos, lo)
             pos = max(pos, hi)
-        for w in self._pending:
-            w.wait()
-        self._pending, self._reduced = [], []
+        self._reduced = []
         self.bw.on_ready = None
 
-    def optimizer_step(self):
+    def wait_grad_exchange(self):
+        """The compute stream waits for every launched bucket (a stream dependency under RCCL)."""
+        for w in getattr(self, "_pending", []):
+            w.wait()
+        self._pending, self._reduced = [], []
+
+    def all_reduce_grads(self):
+        """DDP mean over ranks: launch what is left of the exchange, then wait for all of it."""
+        self.launch_grad_exchange()
+        self.wait_grad_exchange()
+
+    def _apply_update(self, lr, t):
         s = self.s
-        self.all_reduce_grads()
+        self.wait_grad_exchange()
         g = s.grad
         F.l2norm(g, self.norm, self.ws)
-        lr = self.lr_at(self.step)
         for lo, hi, wd in self.runs:
             F.adamw(s.store.p32[lo:hi], g[lo:hi], self.m_buf[lo:hi], self.v_buf[lo:hi], s.store.p16[lo:hi], lr,
-                    self.b1, self.b2, self.eps, wd, self.step + 1, self.norm, self.max_grad_norm)
+                    self.b1, self.b2, self.eps, wd, t, self.norm, self.max_grad_norm)
+
+    def optimizer_step(self):
+        """Clip + AdamW on the exchanged gradient.  With overlap_update the exchange is launched here and the
+        update is applied by the next flush() (the next train_step, after its encoder forward); `self.norm`
+        holds the clipped-over norm once it has run."""
+        lr, t = self.lr_at(self.step), self.step + 1
         self.step += 1
+        self.launch_grad_exchange()
+        if self.overlap_update:
+            self._update = (lr, t)
+        else:
+            self._apply_update(lr, t)
         return self.norm
+
+    def flush(self):
+        """Apply a deferred update (no-op without one).  Call before reading weights or optimizer state."""
+        if self._update is not None:
+            lr, t = self._update
+            self._update = None
+            self._apply_update(lr, t)
 
     # ------------------------------------------------------------------ checkpoint state
     def state_dict(self):
+        self.flush()
         return {"step": self.step, "exp_avg": self.m_buf, "exp_avg_sq": self.v_buf}
 
     def load_state_dict(self, st):
+        self.flush()
         self.step = int(st["step"])
         self.m_buf.copy_(st["exp_avg"])
         self.v_buf.copy_(st["exp_avg_sq"])
@@ -274,6 +315,7 @@ class DistillationTrainer:
 
     def optimizer_state_dict(self):
         """torch.optim.AdamW.state_dict() of the reference's optimizer (tw/checkpoint.py groups)."""
+        self.flush()
         from .checkpoint import optimizer_groups
         g0, g1 = optimizer_groups(self.s.config, self.freeze_encoder, self.freeze_decoder)
         state, idx = {}, 0
@@ -296,6 +338,7 @@ class DistillationTrainer:
 
     def load_optimizer_state_dict(self, sd):
         """Inverse of optimizer_state_dict (also accepts the reference's own optimizer.bin)."""
+        self.flush()
         from .checkpoint import optimizer_groups
         g0, g1 = optimizer_groups(self.s.config, self.freeze_encoder, self.freeze_decoder)
         order = g0 + g1
@@ -327,6 +370,7 @@ class DistillationTrainer:
 
     def save_state(self, output_dir, save_teacher=True, rank=0):
         """accelerator.save_state layout (tw/checkpoint.py)."""
+        self.flush()
         from safetensors.torch import save_file
         os.makedirs(output_dir, exist_ok=True)
         if rank == 0:
@@ -342,6 +386,7 @@ class DistillationTrainer:
     def load_state(self, input_dir):
         """accelerator.load_state(dir) equivalent: student weights, optimizer moments and step.
         Files are read with safe loaders only (safetensors; torch.load(weights_only=True))."""
+        self.flush()
         from safetensors.torch import load_file
         sd = load_file(os.path.join(input_dir, "model.safetensors"))
         sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}

@@ -309,6 +309,7 @@ def main(argv=None):
             if cur_step >= total:
                 break
         epoch += 1
+    trainer.flush()                                          # a deferred last update (DP overlap)
     if rank == 0:
         student.save_pretrained(args.output_dir)
     if world > 1:

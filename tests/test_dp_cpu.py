@@ -52,7 +52,8 @@ def _worker_allreduce(rank, world, port, out):
     # power-of-two world: the trainer folds 1/world into the loss gradient; otherwise the exchange scales
     st.s.grad = local / world if fold else local.clone()
     st.world, st.pg, st.bucket, st.fold_world = world, dist.group.WORLD, 3001, fold
-    st._launch = types.MethodType(DistillationTrainer._launch, st)
+    for name in ("_launch", "launch_grad_exchange", "wait_grad_exchange"):
+        setattr(st, name, types.MethodType(getattr(DistillationTrainer, name), st))
     # two "layers" finished during the backward start their exchange early (out of order, uneven
     # sizes); all_reduce_grads then covers the gaps and waits for everything
     st._pending, st._reduced = [], []
@@ -164,3 +165,49 @@ def test_eval_gather_drops_even_batches_duplicates():
         preds, labels = out[r]
         assert [p[0] for p in preds] == list(range(11))
         assert labels == [[i] for i in range(11)]
+
+
+def _worker_deferred(rank, world, port, out):
+    """optimizer_step with overlap_update launches the exchange and applies nothing; flush() waits for it
+    and applies clip + AdamW once with the step's own lr / t; a second flush is a no-op."""
+    import sys
+    import types
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "taiwan-whisper_amd"))
+    import tw.distill as D
+    _init(rank, world, port)
+    calls = []
+    D.F = types.SimpleNamespace(l2norm=lambda g, norm, ws: (calls.append(("norm", g.clone())), norm.fill_(float(g.norm()))),
+                                adamw=lambda p32, g, m, v, p16, lr, b1, b2, eps, wd, t, norm, mx:
+                                calls.append(("adamw", lr, t)))
+
+    class Stub:
+        pass
+    st = D.DistillationTrainer.__new__(D.DistillationTrainer)
+    st.s, st.bw = Stub(), Stub()
+    st.s.grad = torch.full((5000,), float(rank + 1))
+    st.s.store = Stub()
+    st.s.store.p32 = st.s.store.p16 = torch.zeros(5000)
+    st.m_buf, st.v_buf = torch.zeros(5000), torch.zeros(5000)
+    st.world, st.pg, st.bucket, st.fold_world = world, dist.group.WORLD, 1024, True
+    st.norm, st.ws = torch.zeros(1), torch.zeros(8)
+    st.runs = [(0, 5000, 0.0)]
+    st.lr, st.warmup, st.sched, st.step = 1e-3, 0, "constant", 4
+    st.b1 = st.b2 = st.eps = st.wd = 0.0
+    st.max_grad_norm = 1.0
+    st.overlap_update, st._update = True, None
+    st._pending, st._reduced = [], []
+    st.optimizer_step()
+    assert calls == [] and st._update == (1e-3, 5) and st.step == 5 and len(st._pending) == 5
+    st.flush()
+    assert [c[0] for c in calls] == ["norm", "adamw"] and calls[1][1:] == (1e-3, 5)
+    assert torch.equal(calls[0][1], torch.full((5000,), 3.0))     # the exchanged (summed) gradient
+    st.flush()
+    assert len(calls) == 2 and st._update is None
+    out[rank] = True
+    dist.destroy_process_group()
+
+
+def test_deferred_update_control_flow():
+    out = mp.Manager().dict()
+    mp.spawn(_worker_deferred, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert out[0] and out[1]

@@ -99,3 +99,47 @@ def test_dp_two_ranks_equal_accumulation():
     d_dp, d_acc = p0 - init.cpu(), ref - init.cpu()
     rel = float((d_dp - d_acc).norm() / d_acc.norm())
     assert rel < 1e-3, rel
+
+
+def _worker_overlap(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    mk, g = _setup()
+    from tw.distill import DistillationTrainer
+    B = g["feats"].shape[0]
+    h = B // world
+    res = {}
+    for overlap in (False, True):
+        s, t = mk(1, torch.float32), mk(2, torch.bfloat16)
+        tr = DistillationTrainer(s, t, learning_rate=1e-3, freeze_encoder=True, dp_bucket_mb=1,
+                                 process_group=torch.distributed.group.WORLD, overlap_update=overlap)
+        for it in range(3):
+            lo = (rank * h + it) % B
+            tr.train_step(_batch(g, lo, lo + min(h, B - lo)))
+            if overlap:
+                assert tr._update is not None        # the update waits for the next step's encoder
+        sd = tr.state_dict()                          # flushes
+        assert tr._update is None and tr.step == 3
+        torch.cuda.synchronize()
+        res[overlap] = (s.store.p32.cpu().clone(), sd["exp_avg"].cpu().clone(), sd["exp_avg_sq"].cpu().clone())
+    out[rank] = res
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_deferred_update_bit_identical():
+    """The deferred update (exchange tail beside the next step's frozen-encoder forward, then clip +
+    AdamW) gives bit-identical weights and moments to the in-step update after 3 steps, on both ranks."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_worker_overlap, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        a, b = out[r][False], out[r][True]
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    assert torch.equal(out[0][True][0], out[1][True][0])
