@@ -214,6 +214,21 @@ int tw_kv_head_major(const void* src, int64_t ld, void* dst, int B, int Tk, int 
 int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n, int dtype,
                  const int* t_dev, tw_stream_t stream);
 int tw_step_advance(int* t_dev, int by, tw_stream_t stream);
+/* tw_decoder_layers: every decoder layer of one greedy step at batch B <= 8 in ONE persistent launch (one
+ * 256-thread workgroup per CU, the stages separated by grid barriers) -- replaces the ~10 launches per layer of
+ * the tw_gemv_* / tw_decode_attn sequence that HF generate's per-token WhisperDecoder forward maps to
+ * (generation_whisper.py greedy loop via run_eval.py:680; modeling_whisper.py WhisperDecoderLayer), with
+ * identical arithmetic (the same device bodies).  layers: device table of L entries of 21 pointers each, in
+ * order ln1_w, ln1_b (fp32), wqkv [3d][d], bqkv, wo, bo, ln2_w, ln2_b, wq, bq, cross K, cross V (head-major
+ * [B*H][Tk][64], tw_kv_head_major), wco, bco, ln3_w, ln3_b, w1 [ffn][d], b1, w2 [d][ffn], b2, self cache
+ * [B][T_max][2d] (k | v); x [B][d] the 16-bit residual stream (in/out), qkv [B][3d], o / q [B][d],
+ * h [B][ffn] scratch; part >= B*H*ceil(Tk/128)*66 floats; t_dev = the step index (cache row t, self-attention
+ * over rows 0..t); sync = 8 words, 16-B aligned (words 0-3: the arrival counter, zeroed by the call; word 4:
+ * a sticky error word the caller zeroes once -- nonzero after a barrier timeout).  dtype bf16 or fp16 (code 2);
+ * H * 64 == d, d and ffn multiples of 256.  TW_EUNSUPPORTED when the workgroups cannot all be resident. */
+int tw_decoder_layers(const void* layers, int L, void* x, void* qkv, void* o, void* q, void* h, float* part, int B,
+                      int d, int H, int ffn, int T_max, int Tk, const int* t_dev, float eps, float scale,
+                      unsigned* sync, int dtype, tw_stream_t stream);
 
 /* ---- fp32 arithmetic path (mixed_precision = "no", run_distillation.py:815-823: the reference's default
  * --dtype float32; the fp32 greedy decode pinned token-for-token to HF fp32 generate).  Exact-fp32 MFMA

@@ -111,7 +111,16 @@ constexpr float NEG_BIG = -1e30f;
 // ------------------------------------------------------------------------------------
 // H = false: bf16 Q/K/V/O (autocast); H = true: fp16 (the fp16 decode path: P rounded to fp16 for PV,
 // as SDPA's fp16 flash kernel rounds it)
-template <bool H>
+// LZ = true: lazy max.  A tile is exponentiated against the running max m without computing its own max;
+// a lane whose partial sum of the 16 weights of one query leaves [0, LZ_TH] (a score more than
+// log2(LZ_TH / 16) = 4 above m in the log2 domain, the first tile against m = -1e30, or a NaN) sends the
+// wave down the exact path: S recomputed from the K tile still in LDS (the weights overwrote it), the tile
+// max, the O / l rescale, the weights again.  Weights are then <= LZ_TH before normalisation: bf16 / fp16
+// round them with the same relative precision, and m + log2(l) is the same LSE.  Saves the per-tile
+// max tree (~26 VALU) and the O rescale (~20 VALU when some row max of the wave grew).
+constexpr float LZ_TH = 256.f;
+
+template <bool H, bool LZ>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // [2 stages][K, V]
   const int lane = lane_id(), wave = wave_id_uniform();
@@ -152,29 +161,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     stage_tile(Kb + (int64_t)k0 * p.ldk, p.ldk, p.Tk - k0, Ks, wave, lane);
     stage_tile(Vb + (int64_t)k0 * p.ldv, p.ldv, p.Tk - k0, Ks + TB, wave, lane);
   };
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    const char* Ks = smem + cur * 2 * TB;
-    const char* Vs = Ks + TB;
-    // all K and V fragments of this tile into registers BEFORE the next tile's LDS-DMA is
-    // issued: otherwise the compiler cannot prove the DMA does not alias these reads and
-    // drains vmcnt(0) in the middle of the tile (exposing the whole load latency)
-    bf16x8 kf[4][2], vf[4][2];
-#pragma unroll
-    for (int kj = 0; kj < 4; ++kj)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) kf[kj][kk] = rd_row(Ks, kj * 16, kk, lane);
-#pragma unroll
-    for (int hj = 0; hj < 4; ++hj)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) vf[hj][ss] = rd_tr(Vs, hj * 16, ss, lane);
-    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
-    // S^T = K Q^T
-    f32x4 s[4][2];
+  // S^T = K Q^T for one tile, boundary tiles masked (key tail / causal diagonal)
+  auto scores = [&](const bf16x8 (&kf)[4][2], f32x4 (&s)[4][2], int k0) {
 #pragma unroll
     for (int kj = 0; kj < 4; ++kj) {
       s[kj][0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -185,10 +173,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
         s[kj][1] = mma16<H>(kf[kj][kk], qf[1][kk], s[kj][1]);
       }
     }
-    // online softmax (log2 domain), per query column.  Masking only on boundary tiles
-    // (key tail / causal diagonal); max on raw scores (scale > 0); p = exp2(s*c - m) is one
-    // FMA + one exp; O is rescaled only when some row max of this wave grew.
-    const int k0 = kt * KT;
     const bool need_mask = (k0 + KT > p.Tk) || (p.causal && k0 + KT - 1 > qw + off);
     if (need_mask) {
 #pragma unroll
@@ -204,6 +188,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
           }
       }
     }
+  };
+  // online softmax (log2 domain), per query column: max on raw scores (scale > 0); p = exp2(s*c - m) is
+  // one FMA + one exp; O is rescaled only when some row max of this wave grew.  Returns the lane-partial
+  // sums of the weights (added to l by the caller).
+  auto exact = [&](f32x4 (&s)[4][2], float (&ls)[2]) {
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
       // row max: a tree over the lane's 16 scores, then across the 4 lanes of the query column
@@ -227,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
         for (int hj = 0; hj < 4; ++hj) o[hj][qi] *= alpha;
       }
       m[qi] = mn;
-      float ls = 0.f;      // sequential (a 4-way split moved the micro-config KL by 1e-3 vs the oracle)
+      float a = 0.f;      // sequential (a 4-way split moved the micro-config KL by 1e-3 vs the oracle)
       // s*c - m as one scalar v_fma_f32 per score (a v_pk_fma_f32 costs more issue cycles than two
       // v_fma_f32 beside MFMAs: MI355X_MICROARCH constants table), then v_exp_f32 on it directly
       const float nm = -mn;
@@ -237,10 +226,72 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) {
           const float e = __builtin_amdgcn_exp2f(fmaf(s[kj][qi][r], p.scale_log2, nm));
           s[kj][qi][r] = e;
-          ls += e;
+          a += e;
         }
-      l[qi] += ls;
+      ls[qi] = a;
     }
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const char* Ks = smem + cur * 2 * TB;
+    const char* Vs = Ks + TB;
+    // all K and V fragments of this tile into registers BEFORE the next tile's LDS-DMA is
+    // issued: otherwise the compiler cannot prove the DMA does not alias these reads and
+    // drains vmcnt(0) in the middle of the tile (exposing the whole load latency)
+    bf16x8 kf[4][2], vf[4][2];
+#pragma unroll
+    for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) kf[kj][kk] = rd_row(Ks, kj * 16, kk, lane);
+#pragma unroll
+    for (int hj = 0; hj < 4; ++hj)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) vf[hj][ss] = rd_tr(Vs, hj * 16, ss, lane);
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    const int k0 = kt * KT;
+    f32x4 s[4][2];
+    scores(kf, s, k0);
+    float ls[2];
+    if constexpr (LZ) {
+      // the first tile takes the exact path directly (m = -1e30 would send it there anyway, after a wasted pass)
+      bool fast = kt > 0;
+      if (fast) {
+        // against the running max, no tile max
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) {
+          const float nm = -m[qi];
+          float a = 0.f;
+#pragma unroll
+          for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float e = __builtin_amdgcn_exp2f(fmaf(s[kj][qi][r], p.scale_log2, nm));
+              s[kj][qi][r] = e;
+              a += e;
+            }
+          ls[qi] = a;
+        }
+        if (__any(!(ls[0] <= LZ_TH) || !(ls[1] <= LZ_TH))) {
+          // exact path (rare past the first tile): the K fragments again from this tile's LDS image
+          fast = false;
+          bf16x8 kf2[4][2];
+#pragma unroll
+          for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) kf2[kj][kk] = rd_row(Ks, kj * 16, kk, lane);
+          scores(kf2, s, k0);
+        }
+      }
+      if (!fast) exact(s, ls);
+    } else {
+      exact(s, ls);
+    }
+    l[0] += ls[0];
+    l[1] += ls[1];
     // O^T += V^T P^T
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
@@ -799,7 +850,8 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
   static const int variant = [] {
-    // A/B benchmarking only: 0 = 16x16 kernel (default: fastest measured, tools/bench_attn.py r01),
+    // A/B benchmarking only: 0 = 16x16 kernel with the lazy max (default: enc self 1066 -> 1033 us, cross
+    // 363 -> 349 us against 1, tools/bench_attn.py r03), 1 = the 16x16 kernel with the per-tile max,
     // 4 / 8 = software-pipelined lazy-max 32x32 kernel with that many waves per workgroup
     const char* e = getenv("TW_ATTN_FWD");
     return e ? atoi(e) : 0;
@@ -808,8 +860,10 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
     hipLaunchKernelGGL(attn_fwd32_kernel<4>, dim3((Tq + 127) / 128, B * H), dim3(256), 0, stream, p);
   } else if (variant == 8) {
     hipLaunchKernelGGL(attn_fwd32_kernel<8>, dim3((Tq + 255) / 256, B * H), dim3(512), 0, stream, p);
+  } else if (variant == 1) {
+    hipLaunchKernelGGL((attn_fwd_kernel<false, false>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   } else {
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((attn_fwd_kernel<false, true>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   }
   TW_CHECK_LAUNCH();
   return TW_OK;
@@ -828,7 +882,7 @@ extern "C" int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
-  hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((attn_fwd_kernel<true, false>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -17,6 +17,7 @@
 // The MFMA is issued with operands swapped (Bfrag, Afrag) so each lane ends up holding
 // 4 consecutive output columns of one row: 8/16-B stores in the epilogue.
 #include "gemm_impl.h"
+#include "gemv_impl.h"
 
 
 namespace {
@@ -405,27 +406,6 @@ void launch(GemmP p, int batch, hipStream_t stream) {
 // once per step), A fragments from L2 (A is at most 128 x K bf16), MFMA 16x16x32 with swapped
 // operands, the 4 wave partials summed through LDS, then the per-element epilogue (every flag).
 // ---------------------------------------------------------------------------------------------
-// the epilogue value of C[m][n] (writes the GELU pre-activation to aux on the way), before the store
-template <bool H>
-__device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v) {
-  const int flags = p.flags;
-  v *= p.alpha;
-  if (flags & F_BIAS) v += e2f<H>(p.bias[n]);
-  if (flags & F_ROUND) v = rnd<H>(v);
-  if (flags & F_DGELU) v = rnd<H>(v * gelu_erf_grad(e2f<H>(p.aux[(int64_t)m * p.ldaux + n])));
-  if (flags & F_GELU) {
-    if (flags & F_AUX_OUT) p.aux[(int64_t)m * p.ldaux + n] = f2e<H>(v);
-    v = rnd<H>(gelu_of<H>(v));
-  }
-  if (flags & F_RES) {
-    const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
-    v += ld16_as_f32<H>(p.res, p.res_dtype, (int64_t)mr * p.ldr + n);
-  }
-  if (flags & F_ACCUM) v += ld16_as_f32<H>(p.C, p.c_dtype, (int64_t)m * p.ldc + n);
-  if (flags & F_CLAMP16) v = clamp_f16_stream(rnd<H>(v));
-  return v;
-}
-
 template <bool H>
 __device__ __forceinline__ void epi_element(const GemmP& p, int m, int n, float v) {
   v = epi_value<H>(p, m, n, v);
@@ -545,155 +525,21 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(GemmP p, int S) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// GEMV for the batch-1 (and up to 4-row) decode step: one output column per wave, 4 per workgroup
-// (N / 4 workgroups: 320 for N = 1280, where the 16-column skinny kernel has 80).  The A rows go to LDS
-// first -- as given, or through the LayerNorm in front of the Linear (ln_w != nullptr: the pre-LN residual
-// stream x in, the same half-wave statistics, order and bf16 output as ln_fwd_bf16_kernel, so A is
-// bit-identical to tw_layernorm_fwd's output) -- then each wave streams its W row (16 B per lane, up to
-// 4 loads in flight) against the LDS rows, fp32 FMAs in k order per lane, one butterfly sum, and lane 0
-// applies the full epilogue (epi_element).  Fusing the LN removes one launch per LN'd Linear, which is
-// most of a batch-1 step's cost (every launch there is latency-bound).
-// ---------------------------------------------------------------------------------------------
-// Optional KV-cache append fused into the epilogue (the decode step's QKV projection): output columns
-// n >= kv.col0 are also stored at kv.cache[m * kv.sb + (*kv.t) * kv.ld + n - kv.col0] -- what tw_kv_append
-// copies, one launch fewer per decoder layer.
-struct GemvKV {
-  void* cache;
-  int64_t sb, ld;
-  int col0;
-  const int* t;
-};
-
+// GEMV for the batch <= 8 decode step: the body (LN staging, column dots, epilogue) lives in gemv_impl.h,
+// shared with the persistent decoder-step kernel (decode_step.hip)
 template <bool H, int MR, int CPW, int PRE>
 __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                    float eps, GemvKV kv) {
   extern __shared__ __attribute__((aligned(16))) char gemv_smem[];
   bf16* xs = (bf16*)gemv_smem;                         // [MR][K] bf16
   const int lane = lane_id(), wave = wave_id_uniform();
-  const int K = p.K;
-  // this wave's W rows (CPW output columns): the first (up to) PRE 16-B pieces per lane are loaded before
-  // the A rows are staged, so their HBM latency hides behind the LayerNorm / LDS prologue.  PRE is sized to
-  // K (3 pieces cover K = 1280, 10 cover 5120): more registers would cut the waves per SIMD, and the
-  // 1280-workgroup fc1 GEMV needs 5 per SIMD to run in one round (measured: 9.6 -> 13.8 us at PRE = 12)
-  constexpr int GV_PRE = PRE;
   const int n0 = (blockIdx.x * 4 + wave) * CPW;
-  bf16x8 wpre[CPW][GV_PRE];
-  const int npre = min(GV_PRE, (K - lane * 8 + 511) / 512);
-#pragma unroll
-  for (int c = 0; c < CPW; ++c) {
-    const int n = n0 + c;
-    const bf16* wr = p.B + (int64_t)(n < p.N ? n : 0) * p.ldb;
-#pragma unroll
-    for (int u = 0; u < GV_PRE; ++u) wpre[c][u] = (u < npre) ? *(const bf16x8*)(wr + lane * 8 + u * 512) : bf16x8{};
-  }
-  // wave w stages rows w, w + 4 (MR = 8: the batched-fallback decode of up to 8 rows)
-  for (int row = wave; row < MR; row += 4) {
-    bf16* dst = xs + (int64_t)row * K;
-    if (row >= p.M) {
-      for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = bf16x8{};
-    } else if (lnw) {
-      const bf16* xr = p.A + (int64_t)row * p.lda;
-      const int hl = lane & 31, nch = K / 256;
-      float s = 0.f;
-      for (int c = 0; c < nch; ++c) {
-        const bf16x8 t = *(const bf16x8*)(xr + (c * 32 + hl) * 8);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s += e2f<H>(t[q]);
-      }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      const float mean = s / K;
-      float ss = 0.f;
-      for (int c = 0; c < nch; ++c) {
-        const bf16x8 t = *(const bf16x8*)(xr + (c * 32 + hl) * 8);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[q]) - mean; ss += d * d; }
-      }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-      const float rstd = rsqrtf(ss / K + eps);
-      if (lane < 32) {
-        for (int c = 0; c < nch; ++c) {
-          const int e = (c * 32 + hl) * 8;
-          const bf16x8 t = *(const bf16x8*)(xr + e);
-          const f32x4 w0 = *(const f32x4*)(lnw + e), w1 = *(const f32x4*)(lnw + e + 4);
-          const f32x4 b0 = *(const f32x4*)(lnb + e), b1 = *(const f32x4*)(lnb + e + 4);
-          float v[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = e2f<H>(t[q]);
-          bf16x8 o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            o[q] = f2e<H>((v[q] - mean) * rstd * w0[q] + b0[q]);
-            o[q + 4] = f2e<H>((v[q + 4] - mean) * rstd * w1[q] + b1[q]);
-          }
-          *(bf16x8*)(dst + e) = o;
-        }
-      }
-    } else {
-      const bf16* xr = p.A + (int64_t)row * p.lda;
-      for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = *(const bf16x8*)(xr + e);
-    }
-  }
+  bf16x8 wpre[CPW][PRE];
+  gemv_preload<H, CPW, PRE>(p, n0, lane, wpre);
+  gemv_stage_rows<H, MR>(p, lnw, lnb, eps, xs, wave, 4, lane);
   __syncthreads();
   if (n0 >= p.N) return;
-  float acc[CPW][MR];
-#pragma unroll
-  for (int c = 0; c < CPW; ++c)
-#pragma unroll
-    for (int r = 0; r < MR; ++r) acc[c][r] = 0.f;
-  // k order per lane: pieces u = 0, 1, ... at k = lane*8 + 512u (the preloaded ones first, the rest streamed)
-#pragma unroll
-  for (int u = 0; u < GV_PRE; ++u) {
-    if (u < npre) {
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + lane * 8 + u * 512);
-#pragma unroll
-        for (int c = 0; c < CPW; ++c)
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(e2f<H>(wpre[c][u][q]), e2f<H>(a8[q]), acc[c][r]);
-      }
-    }
-  }
-  for (int k0 = lane * 8 + GV_PRE * 512; k0 < K; k0 += 512) {
-#pragma unroll
-    for (int c = 0; c < CPW; ++c) {
-      const int n = n0 + c;
-      const bf16x8 w8 = *(const bf16x8*)(p.B + (int64_t)(n < p.N ? n : 0) * p.ldb + k0);
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + k0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(e2f<H>(w8[q]), e2f<H>(a8[q]), acc[c][r]);
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < CPW; ++c)
-#pragma unroll
-    for (int r = 0; r < MR; ++r) acc[c][r] = wave_sum(acc[c][r]);
-  if (lane == 0) {
-    const int64_t t = kv.cache ? (int64_t)*kv.t : 0;
-#pragma unroll
-    for (int c = 0; c < CPW; ++c)
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        const int n = n0 + c;
-        if (r < p.M && n < p.N) {
-          const float v = epi_value<H>(p, r, n, acc[c][r]);
-          const int64_t co = (int64_t)r * p.ldc + n;
-          if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
-          else ((float*)p.C)[co] = v;
-          if (kv.cache && n >= kv.col0) {
-            const int64_t ko = r * kv.sb + t * kv.ld + (n - kv.col0);
-            if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2e<H>(v);
-            else ((float*)kv.cache)[ko] = v;
-          }
-        }
-      }
-  }
+  gemv_finish<H, MR, CPW, PRE>(p, kv, xs, n0, lane, wpre);
 }
 
 // Row blocks per skinny launch: batches of 65..128 rows run as 2 blocks of 64 (blockIdx.z) -- the

@@ -56,6 +56,7 @@ SIGNATURES = {
     "tw_kv_append": [P, I64, P, I64, I64, I32, I32, I32, P, P],
     "tw_kv_head_major": [P, I64, P, I32, I32, I32, I32, P],
     "tw_step_advance": [P, I32, P],
+    "tw_decoder_layers": [P, I32, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, P, F32, F32, P, I32, P],
     # fp16 arithmetic path (torch_dtype=float16 decode: run_eval.py:99, run_pseudo_labelling.py:461-463)
     "tw_gemm_f16": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I32, I64, I64, I64, F32, P,
                     P, I64, I64, I32, I32, P, I64, I64, I32, P],

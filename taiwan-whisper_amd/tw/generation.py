@@ -31,6 +31,9 @@ import torch
 from . import ops as F
 
 _XKV_HEAD_MAJOR = os.environ.get("TW_XKV_HEAD_MAJOR", "1") != "0"
+# batch <= 8: every decoder layer of a step in one persistent launch (tw_decoder_layers, csrc/decode_step.hip);
+# TW_DECODE_MEGA=0 keeps the per-Linear / per-attention launches (A/B runs; the tests compare the two)
+MEGA = os.environ.get("TW_DECODE_MEGA", "1") != "0"
 
 
 class DecodeSession:
@@ -74,6 +77,11 @@ class DecodeSession:
         # separate LayerNorm
         self.gemv = B <= 8 and model.compute in ("bf16", "fp16") and d % 256 == 0
         self.gemv_ln = self.gemv and model.stream_dtype == act
+        # the persistent decoder-step kernel takes the same operands as the GEMV path (16-bit stream, LN fused,
+        # head-major cross K/V); a per-layer pointer table, the cross-attention partials and the barrier words
+        self.mega = MEGA and self.gemv_ln and self.hm and cfg.decoder_ffn_dim % 256 == 0
+        if self.mega:
+            self._build_layer_table()
 
     def set_encoder(self, enc16):
         """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe).  enc16 holds B*Tk
@@ -103,6 +111,34 @@ class DecodeSession:
             else:
                 m._lin(enc16, wkv, bkv, kv)
         del proj
+
+    def _build_layer_table(self):
+        m, B, d, H, Tk = self.m, self.B, self.d, self.H, self.Tk
+        rows = []
+        for i in range(m.config.decoder_layers):
+            p = f"model.decoder.layers.{i}"
+            kv = self.cross_kv[i]
+            hv = B * H * Tk * 64
+            ts = [m.ln_param(p + ".self_attn_layer_norm.weight"), m.ln_param(p + ".self_attn_layer_norm.bias"),
+                  m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d)),
+                  m.wspan(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,)),
+                  m._w16(p + ".self_attn.out_proj.weight"), m._w16(p + ".self_attn.out_proj.bias"),
+                  m.ln_param(p + ".encoder_attn_layer_norm.weight"), m.ln_param(p + ".encoder_attn_layer_norm.bias"),
+                  m._w16(p + ".encoder_attn.q_proj.weight"), m._w16(p + ".encoder_attn.q_proj.bias"),
+                  kv, kv[hv:],
+                  m._w16(p + ".encoder_attn.out_proj.weight"), m._w16(p + ".encoder_attn.out_proj.bias"),
+                  m.ln_param(p + ".final_layer_norm.weight"), m.ln_param(p + ".final_layer_norm.bias"),
+                  m._w16(p + ".fc1.weight"), m._w16(p + ".fc1.bias"), m._w16(p + ".fc2.weight"),
+                  m._w16(p + ".fc2.bias"), self.self_kv[i]]
+            rows.append([t.data_ptr() for t in ts])
+        self._ltab = torch.tensor(rows, dtype=torch.int64).view(-1).to(m.device)
+        self._part = torch.empty(B * H * ((Tk + 127) // 128) * 66, dtype=torch.float32, device=m.device)
+        self._sync = torch.zeros(8, dtype=torch.int32, device=m.device)
+
+    def check(self):
+        """Raise if a persistent decoder-step launch gave up at a grid barrier (its sticky error word)."""
+        if self.mega and int(self._sync[4].item()) != 0:
+            raise RuntimeError("tw_decoder_layers: a grid barrier timed out (workgroups not co-resident?)")
 
     def _ln(self, x, name):
         m = self.m
@@ -142,7 +178,10 @@ class DecodeSession:
         x, o, t_dev = self.x, self.o, self.t_dev
         F.embed_step(self.cur, E, Pe, x, t_dev, T_max)
         sb = T_max * 2 * d
-        for i in range(m.config.decoder_layers):
+        if self.mega:
+            F.decoder_layers(self._ltab, m.config.decoder_layers, x, self.qkv, o, self.q, self.h, self._part, B, d, H,
+                             m.config.decoder_ffn_dim, T_max, self.Tk, t_dev, 1e-5, 0.125, self._sync)
+        for i in range(0 if self.mega else m.config.decoder_layers):
             p = f"model.decoder.layers.{i}"
             # self attention: fused QKV -> staging; k, v appended at row t of the cache
             wqkv = m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d))
@@ -318,6 +357,7 @@ class _Decoder:
             t += 1
             if (t - P) % 8 == 7 and bool(sel.done.all()):
                 break
+        sess.check()
         gen = sel.ids[:, P:t + 1]
         # trim trailing columns in which every row had already finished (HF stops at the step
         # where the last row emits eos)

@@ -516,6 +516,25 @@ def kv_head_major(src, ld, dst, B, Tk, H):
     call("tw_kv_head_major", src.data_ptr(), ld, dst.data_ptr(), B, Tk, H, _dt(src), _stream())
 
 
+def decoder_layers(table, L, x, qkv, o, q, h, part, B, d, H, ffn, T_max, Tk, t_dev, eps, scale, sync):
+    """tw_decoder_layers: every decoder layer of one greedy step (B <= 8) in one persistent launch
+    (include/tw_hip.h).  table: int64 [L * 21] device pointers (see the header for their order)."""
+    dt = x.dtype
+    assert dt in HALF and all(t.dtype == dt for t in (qkv, o, q, h)), "decoder_layers: 16-bit buffers"
+    assert table.dtype == torch.int64 and table.is_cuda and table.numel() == L * 21
+    assert part.dtype == torch.float32 and sync.dtype == torch.int32 and sync.numel() >= 8
+    assert t_dev.dtype == torch.int32 and 1 <= B <= 8 and H * 64 == d
+    _need(x, B * d, "decoder_layers x")
+    _need(qkv, B * 3 * d, "decoder_layers qkv")
+    _need(o, B * d, "decoder_layers o")
+    _need(q, B * d, "decoder_layers q")
+    _need(h, B * ffn, "decoder_layers h")
+    _need(part, B * H * ((Tk + 127) // 128) * 66, "decoder_layers part")
+    call("tw_decoder_layers", table.data_ptr(), L, x.data_ptr(), qkv.data_ptr(), o.data_ptr(), q.data_ptr(),
+         h.data_ptr(), part.data_ptr(), B, d, H, ffn, T_max, Tk, t_dev.data_ptr(), float(eps), float(scale),
+         sync.data_ptr(), _dt(x), _stream())
+
+
 def step_advance(t_dev, by=1):
     assert t_dev.dtype == torch.int32 and t_dev.is_cuda
     call("tw_step_advance", t_dev.data_ptr(), int(by), _stream())
