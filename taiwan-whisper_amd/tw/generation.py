@@ -31,9 +31,11 @@ import torch
 from . import ops as F
 
 _XKV_HEAD_MAJOR = os.environ.get("TW_XKV_HEAD_MAJOR", "1") != "0"
-# batch <= 8: every decoder layer of a step in one persistent launch (tw_decoder_layers, csrc/decode_step.hip);
-# TW_DECODE_MEGA=0 keeps the per-Linear / per-attention launches (A/B runs; the tests compare the two)
-MEGA = os.environ.get("TW_DECODE_MEGA", "1") != "0"
+# batch <= 8: every decoder layer of a step in one persistent launch (tw_decoder_layers, csrc/decode_step.hip),
+# opt-in with TW_DECODE_MEGA=1: bit-identical to the per-launch step (tests/test_decode_step_gpu.py) but measured
+# slower on c5 (1.79 vs 1.08 ms per decode step, profiles/r03_v1_c5_*.log): a grid barrier + its acquire cost more
+# than the graph-replayed kernel boundary it replaces
+MEGA = os.environ.get("TW_DECODE_MEGA", "0") == "1"
 
 
 class DecodeSession:
