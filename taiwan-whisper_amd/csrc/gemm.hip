@@ -823,14 +823,15 @@ int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
 void* tw_device_workspace(hipStream_t stream, size_t bytes) { return splitk_workspace(stream, bytes); }
 
-// Which implementation tw_gemm_bf16 runs for a call of this shape: 0 = the kernels of this file, 1 = hipBLASLt
-// (plain forward projections: K-major operands, bf16 output, bias/round only, alpha 1, K <= 2048, M >= 4096,
-// N >= 256, no forced tile).  TW_GEMM_VENDOR=0 keeps everything on the own kernels (A/B runs).
+// Which implementation tw_gemm_bf16 runs for a call of this shape: 0 = the hand-written kernels of this file
+// (every call, by default: BASELINE north_star "no dual backends"), 1 = hipBLASLt, only with TW_GEMM_VENDOR=1 (A/B
+// runs against the vendor library: plain forward projections -- K-major operands, bf16 output, bias/round only,
+// alpha 1, K <= 2048, M >= 4096, N >= 256, no forced tile -- and the MN-major-B backward dX products, K <= 8192).
 extern "C" int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, int c_dtype, int batch, float alpha,
                                int flags) {
   static const int env_vendor = [] {
     const char* e = getenv("TW_GEMM_VENDOR");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   // MN-major B (the dX = dY . W products of the backward) up to K = 8192: hipBLASLt's NN kernels measured
   // 13-30 % faster than the 128x128 kernel (tools/bench_head_bwd.py VENDOR_NN=1)
