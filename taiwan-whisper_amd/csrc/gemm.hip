@@ -903,6 +903,9 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (flags & 512) tile = 256;
   if (flags & 1024) tile = 2561;      // 256x128, 3-stage ring
   if (flags & 2048) tile = 2562;      // 256x256 ping-pong (K-major A and B only)
+  // the fp16 persistent kernel is compiled with the fast full-tile epilogues only (gemm_impl.h epilogue_k):
+  // ragged shapes and the generic epilogue kind take the 128x128 kernel
+  if (H && tile == 2562 && ((M % 256) || (N % 256) || p.epi == EPI_GENERIC)) tile = 128;
   const int64_t ntiles = (tile == 256 || tile == 2562) ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
   // decode-step GEMMs (tools/bench_skinny.py, r01): the weight-streaming kernel wins for N <= 3840
@@ -983,7 +986,9 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
       !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
     int m_dp = 0;
     const int S = sk_tail_plan(p, batch, m_dp);
-    if (S > 0 && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
+    // (fp16: the persistent kernel runs full tiles only, so both parts must be whole 256-row blocks)
+    const bool full = !H || ((N % 256) == 0 && ((M - m_dp * 256) % 256) == 0 && p.epi != EPI_GENERIC);
+    if (S > 0 && full && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
   }
   if constexpr (H) {
     dispatch<true, false, false>(p, batch, stream, tile);

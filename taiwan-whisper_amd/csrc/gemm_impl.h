@@ -307,8 +307,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool H>
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  return __builtin_bit_cast(uint32_t, bf16x2{f2e<H>(a), f2e<H>(b)});
+  if constexpr (H) {
+    // fp16: one v_cvt_pk_f16_f32 (gfx950, RNE) on the two fp32 values, opaque to the compiler, so it cannot fold
+    // the fp32 epilogue arithmetic into a single-rounding v_fma_mixlo_f16 (f2e's reason for its asm barrier)
+    uint32_t r;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+  } else {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    return __builtin_bit_cast(uint32_t, bf16x2{f2e<H>(a), f2e<H>(b)});
+  }
 }
 template <bool H>
 __device__ __forceinline__ float lo_e(uint32_t u) {
@@ -510,10 +518,17 @@ __device__ __forceinline__ void epilogue_k(const GemmP& p, const f32x4 (&acc)[BM
   } else if constexpr (KIND == EPI_GENERIC) {
     epilogue_generic<H, BM, BN, WM, WN, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
   } else {
-    if ((m0 + BM <= p.M) && (n0 + BN <= p.N))
+    if constexpr (H && PB) {
+      // fp16 persistent kernel: full tiles only (the host launches it for M, N multiples of 256).  Compiling
+      // the generic edge-tile epilogue into the fp16 instantiations spilled their accumulators (528 B of
+      // scratch, 3-5x slower on c4's encoder): the fp16 rounding barrier of f2e keeps every per-element path
+      // of that epilogue from folding, and its register demand spills the whole kernel.
       epilogue_fast<H, BM, BN, WM, WN, KIND, MI0, MI1, PB>(p, acc, m0, n0, wm, wn, lane, bz, braw);
-    else
+    } else if ((m0 + BM <= p.M) && (n0 + BN <= p.N)) {
+      epilogue_fast<H, BM, BN, WM, WN, KIND, MI0, MI1, PB>(p, acc, m0, n0, wm, wn, lane, bz, braw);
+    } else {
       epilogue_generic<H, BM, BN, WM, WN, MI0, MI1, true>(p, acc, m0, n0, wm, wn, lane, bz);
+    }
   }
 }
 
