@@ -886,7 +886,14 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   // tools/bench_pp_prio.py with TW_GEMM_GROUP_M); plain row-major elsewhere (K = 5120 and the
   // decoder's M = B x 447 shapes lose with grouping)
   const bool grouped = !a_trans && !b_trans && batch == 1 && M >= 65536 && K <= 2048;
-  p.group_m = env_group > 0 ? env_group : (grouped ? 8 : 1);
+  // TW_GEMM_GROUP_DEC (A/B): runs of that many m-tiles for the decoder's mid-width projections (M < 65536,
+  // 2048 <= N <= 4096: the teacher's fused QKV measured 1025 -> 1119 TF/s with runs of 2, tools/gemm_own_shapes.sh)
+  static const int env_group_dec = [] {
+    const char* e = getenv("TW_GEMM_GROUP_DEC");
+    return e ? atoi(e) : 0;
+  }();
+  const bool dec_mid = !a_trans && !b_trans && batch == 1 && M < 65536 && N >= 2048 && N <= 4096 && K <= 2048;
+  p.group_m = env_group > 0 ? env_group : (grouped ? 8 : (dec_mid && env_group_dec > 0 ? env_group_dec : 1));
   p.epi = pick_epilogue(p, batch);
   // 256x256 tiles (8 waves) when the problem has enough tiles to fill the chip, else 128x128
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;

@@ -34,7 +34,7 @@ import torch
 from . import ops
 from .config import GenerationConfig, WhisperConfig
 
-_DEFER_RES = os.environ.get("TW_DEFER_RES", "1") != "0"
+_DEFER_RES = os.environ.get("TW_DEFER_RES", "1")   # "0": never, "2": fp32 streams only, else default
 
 F = ops
 
@@ -455,9 +455,9 @@ class WhisperForConditionalGeneration:
         the bf16 teacher stream for out_proj only (the plain projection then runs on hipBLASLt; at fc2 the extra
         LN traffic costs what the epilogue saves).  DESIGN.md §5; TW_DEFER_RES=0 disables (A/B runs)."""
         # tw_add_layernorm_fwd: D % 256 == 0 and D <= 1280 (every Whisper size), else the residual epilogue
-        if not _DEFER_RES or self.act_dtype != torch.bfloat16 or self.config.d_model % 256 or self.config.d_model > 1280:
+        if _DEFER_RES == "0" or self.act_dtype != torch.bfloat16 or self.config.d_model % 256 or self.config.d_model > 1280:
             return False
-        return self.stream_dtype == torch.float32 or kind == "attn"
+        return self.stream_dtype == torch.float32 or (kind == "attn" and _DEFER_RES != "2")
 
     def _ln_in(self, x, pend, name, save):
         """Block-entry LayerNorm -> (stream, LN output).  pend: a deferred residual update (bf16), added to
