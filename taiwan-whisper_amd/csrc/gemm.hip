@@ -989,7 +989,14 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (flags & 262144) tile = 2563;
   // (tools/bench_gemm_dec.py: fc2 K = 5120 417 -> 347 us; at K = 1280 the split's fp32 round trip costs
   // more than the third round it saves, 125 -> 140 us, so short K stays on the 128x128 kernel)
-  if (!a_trans && !b_trans && tile == 128 && env_sk && K >= 3072 &&
+  // TW_GEMM_SK_SUB_MINK (A/B): the shortest K for which grids of less than one round of 256-tiles (the 512-clip
+  // decode step's Linears) are split over K on the persistent kernel; whole-round + tail splits keep K >= 3072
+  static const int env_sk_sub_mink = [] {
+    const char* e = getenv("TW_GEMM_SK_SUB_MINK");
+    return e ? atoi(e) : 3072;
+  }();
+  const bool sub_round = (int64_t)((M + 255) / 256) * ((N + 255) / 256) < pp_grid_cus() && M >= 256;
+  if (!a_trans && !b_trans && tile == 128 && env_sk && (K >= 3072 || (sub_round && K >= env_sk_sub_mink)) &&
       !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
     int m_dp = 0;
     const int S = sk_tail_plan(p, batch, m_dp);
