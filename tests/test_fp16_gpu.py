@@ -59,10 +59,12 @@ def _h(x):
 
 # ------------------------------------------------------------------------------------------ kernels
 @pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (8, 1280, 5120), (100, 3840, 1280), (300, 640, 256),
-                                   (512, 1280, 5120), (4480, 1280, 1280), (65536, 1024, 512)])
+                                   (512, 1280, 5120), (4480, 1280, 1280), (65536, 1024, 512), (65636, 1024, 512)])
 def test_gemm_f16_bias_round(M, N, K):
     """Every routing of tw_gemm_f16 (skinny / skinny split-K, 128x128, sub-round split-K, persistent 256x256):
-    fp16 output within 1 ulp of the fp32 product of the same fp16 operands (+ fp16 bias)."""
+    fp16 output within 1 ulp of the fp32 product of the same fp16 operands (+ fp16 bias).  (65636, 1024, 512): a
+    grid the persistent kernel would take but with a ragged last row block -- the fp16 persistent kernel has
+    full-tile epilogues only, so the host must route it to the 128x128 kernel (no write past row M)."""
     from tw import ops
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     A = (torch.randn(M, K, device=DEV, generator=g)).half()
@@ -75,10 +77,12 @@ def test_gemm_f16_bias_round(M, N, K):
     assert float(err.max()) <= 1.0, float(err.max())
 
 
-def test_gemm_f16_gelu_residual_clamp():
+@pytest.mark.parametrize("M", [1500, 65536])
+def test_gemm_f16_gelu_residual_clamp(M):
+    """M = 1500: the 128x128 kernel; M = 65536: the persistent kernel's fp16 GELU / residual + clamp epilogues."""
     from tw import ops
     g = torch.Generator(device=DEV).manual_seed(7)
-    M, N, K = 1500, 1280, 1280
+    N, K = 1280, 1280
     A = torch.randn(M, K, device=DEV, generator=g).half()
     W = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).half()
     b = torch.randn(N, device=DEV, generator=g).half()
