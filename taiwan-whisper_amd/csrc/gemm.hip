@@ -727,6 +727,9 @@ int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
 template <bool H, bool AT, bool BT>
 void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
   if (tile == 2562 && !AT && !BT) launch_pp<H>(p, batch, stream);
+  else if (tile == 1284) {
+    if constexpr (!AT && !BT) launch<H, AT, BT, 128, 128, 2, 2, 4>(p, batch, stream);   // 4-stage ring
+  }
   else if (tile == 256) launch<H, AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
   else if (tile == 2561) launch<H, AT, BT, 256, 128, 4, 2, 3>(p, batch, stream);
   else if (tile == 2563) launch<H, AT, BT, 256, 128, 4, 2, 2>(p, batch, stream);
@@ -1004,6 +1007,16 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     const bool full = !H || ((N % 256) == 0 && ((M - m_dp * 256) % 256) == 0 && p.epi != EPI_GENERIC);
     if (S > 0 && full && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
   }
+  // TW_GEMM_DEEP (A/B): grids of at most one 128x128 tile per CU (the 512-clip decode step's Linears: 40-160
+  // tiles, one workgroup per CU anyway) on a 4-stage ring -- three K-steps in flight instead of one hide the
+  // load latency that bounds a 20-K-step tile
+  static const int env_deep = [] {
+    const char* e = getenv("TW_GEMM_DEEP");
+    return e ? atoi(e) : 0;
+  }();
+  if (env_deep && tile == 128 && !a_trans && !b_trans && !(flags & 256) &&
+      (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch <= pp_grid_cus())
+    tile = 1284;
   if constexpr (H) {
     dispatch<true, false, false>(p, batch, stream, tile);
   } else {
