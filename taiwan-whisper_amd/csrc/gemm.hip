@@ -1007,12 +1007,13 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     const bool full = !H || ((N % 256) == 0 && ((M - m_dp * 256) % 256) == 0 && p.epi != EPI_GENERIC);
     if (S > 0 && full && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
   }
-  // TW_GEMM_DEEP (A/B): grids of at most one 128x128 tile per CU (the 512-clip decode step's Linears: 40-160
-  // tiles, one workgroup per CU anyway) on a 4-stage ring -- three K-steps in flight instead of one hide the
-  // load latency that bounds a 20-K-step tile
+  // Grids of at most one 128x128 tile per CU (the 512-clip decode step's Linears: 40-160 tiles, one workgroup per
+  // CU anyway) run on a 4-stage ring: three K-steps in flight instead of one hide the load latency that bounds a
+  // 20-K-step tile.  Same tile, same K order: bit-identical.  c4 fp16 155.8 -> 158.5 utt/s, c5 16.93 -> 17.09
+  // audio s/s (same box, profiles/r03_s_gemm_deep_ab.log).  TW_GEMM_DEEP=0: the 2-stage kernel (A/B runs).
   static const int env_deep = [] {
     const char* e = getenv("TW_GEMM_DEEP");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   if (env_deep && tile == 128 && !a_trans && !b_trans && !(flags & 256) &&
       (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch <= pp_grid_cus())
