@@ -328,9 +328,31 @@ def load_mfma(workload, family):
     return d.get(workload, {}).get(family, {}).get("mfma_busy_frac")
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` outside a launcher: start N ranks (one per GPU) under torch.distributed.run as a
+    child process -- before this process makes any GPU call -- and return its exit code.  The same command the
+    driver runs: --nnodes 1, --master-addr 127.0.0.1."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    if os.environ.get("TW_BENCH_PRINT_LAUNCH") == "1":          # tests: show the launch, start nothing
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default WORLD_SIZE under a launcher, else 1.  Without a launcher, "
+                         "N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5"])
@@ -349,7 +371,15 @@ def main():
     args.steps = dflt[1] if args.steps is None else args.steps
     args.warmup = dflt[2] if args.warmup is None else args.warmup
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world) if env_world else 1
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks", file=sys.stderr)
+        sys.exit(2)
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # TW_BENCH_REHEARSE=1: all ranks on cuda:0 over gloo (multi-rank rehearsal on a 1-GPU box);
@@ -378,6 +408,7 @@ def main():
     student, teacher, freeze_encoder = make_models(args, device)
     trainer = DistillationTrainer(student, teacher, learning_rate=1e-4, warmup_steps=0,
                                   freeze_encoder=freeze_encoder, process_group=pg)
+    trainer.exchange_events = [] if pg is not None else None     # exposed gradient-exchange waits
     fe = WhisperFeatureExtractor(device=device)
     batches = make_batches(args, device, rank)
 
@@ -390,10 +421,12 @@ def main():
         m = step(i)
     trainer.flush()              # the warmup's last update (deferred under DP) stays outside the timed region
     torch.cuda.synchronize()
+    if trainer.exchange_events is not None:
+        trainer.exchange_events.clear()
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    timer = KernelTimer("gemm_nn", "gemm_nn_lt")
+    timer = KernelTimer("gemm_nn")
     with timer:
         t0 = time.perf_counter()
         for i in range(args.steps):
@@ -410,7 +443,17 @@ def main():
     elapsed = float(elapsed.item())
     loss = float(m["loss"].item())
     ks = timer.summary()
-    ks_lt = timer.summary("gemm_nn_lt")
+    exch_ms = None
+    if trainer.exchange_events is not None:
+        # compute-stream time between reaching the gradient-exchange wait and passing it (the all-reduce time
+        # the step does not hide), per timed step
+        exch_ms = sum(a.elapsed_time(b) for a, b in trainer.exchange_events) / args.steps
+    dist = dict(backend=torch.distributed.get_backend(pg) if pg is not None else None,
+                world_size=torch.distributed.get_world_size(pg) if pg is not None else 1,
+                exchange_exposed_ms_per_step=None if exch_ms is None else round(exch_ms, 3),
+                exchange="bucketed async SUM all-reduce of the flat fp32 student gradient, launched per finished "
+                         "layer during the backward; clip + AdamW deferred under the next encoder forward"
+                if pg is not None else None)
 
     teacher_ms = None
     if not args.no_teacher_fwd:
@@ -447,14 +490,6 @@ def main():
                                "gemm_kernel<false,false,128,...> for grids under ~1000 256-tiles",
                         launches_per_step=ks["launches"] // args.steps, avg_launch_ms=round(ks["avg_ms"], 4),
                         algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4))
-        vendor = None
-        if ks_lt is not None:      # the plain-bias projections routed to hipBLASLt (tw_gemm_backend == 1)
-            vendor = dict(launches_per_step=ks_lt["launches"] // args.steps,
-                          achieved_tflops=round(ks_lt["rate"] / 1e12, 2),
-                          frac=round(ks_lt["rate"] / 1e12 / PEAK_BF16_TFLOPS, 4),
-                          ms_per_step=round(ks_lt["total_ms"] / args.steps, 2),
-                          kernel="hipBLASLt (TN, bias epilogue, bf16 out): QKV / cross-KV / cross-Q / out_proj of fp32 streams (residual "
-                                 "deferred to the next LN) / tied LM head, K <= 2048")
         out = {
             "metric": "distillation utterances/sec (30 s clips)",
             "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
@@ -476,7 +511,7 @@ def main():
             "step_mfma_frac": round(flops_clip * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(loss, 4),
             "roofline": roof,
-            "vendor_gemm": vendor,
+            "distributed": dist,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

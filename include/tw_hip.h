@@ -38,10 +38,6 @@ typedef void* tw_stream_t; /* hipStream_t */
 #define TW_GEMM_TILE256x128 1024  /* force the 256x128 tile with the 3-stage LDS ring */
 #define TW_GEMM_TILE256PP 2048    /* force the 256x256 ping-pong kernel (a_trans = b_trans = 0 only) */
 
-/* Backend tw_gemm_bf16 takes for a call of this shape: 0 = the hand-written kernels (gemm.hip), 1 = hipBLASLt
- * for the plain projections (K-major A, bf16 output, bias / round only, alpha 1, M >= 4096, N >= 256, and
- * K <= 2048 with K-major B or K <= 8192 with MN-major B; csrc/gemm_vendor.hip).  Lets a caller attribute timings; TW_GEMM_VENDOR=0 disables. */
-int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, int c_dtype, int batch, float alpha, int flags);
 
 /* bf16 MFMA GEMM  C[b] = epi(alpha * A[b] . B[b]^T), A [M][K] (a_trans: [K][M]), B [N][K] (b_trans: [K][N]).
  * Replaces every nn.Linear / Conv1d (as GEMM) / tied proj_out matmul of the step, forward and
@@ -214,21 +210,6 @@ int tw_kv_head_major(const void* src, int64_t ld, void* dst, int B, int Tk, int 
 int tw_kv_append(const void* src, int64_t ld_src, void* cache, int64_t ld_row, int64_t sb, int B, int n, int dtype,
                  const int* t_dev, tw_stream_t stream);
 int tw_step_advance(int* t_dev, int by, tw_stream_t stream);
-/* tw_decoder_layers: every decoder layer of one greedy step at batch B <= 8 in ONE persistent launch (one
- * 256-thread workgroup per CU, the stages separated by grid barriers) -- replaces the ~10 launches per layer of
- * the tw_gemv_* / tw_decode_attn sequence that HF generate's per-token WhisperDecoder forward maps to
- * (generation_whisper.py greedy loop via run_eval.py:680; modeling_whisper.py WhisperDecoderLayer), with
- * identical arithmetic (the same device bodies).  layers: device table of L entries of 21 pointers each, in
- * order ln1_w, ln1_b (fp32), wqkv [3d][d], bqkv, wo, bo, ln2_w, ln2_b, wq, bq, cross K, cross V (head-major
- * [B*H][Tk][64], tw_kv_head_major), wco, bco, ln3_w, ln3_b, w1 [ffn][d], b1, w2 [d][ffn], b2, self cache
- * [B][T_max][2d] (k | v); x [B][d] the 16-bit residual stream (in/out), qkv [B][3d], o / q [B][d],
- * h [B][ffn] scratch; part >= B*H*ceil(Tk/128)*66 floats; t_dev = the step index (cache row t, self-attention
- * over rows 0..t); sync = 8 words, 16-B aligned (words 0-3: the arrival counter, zeroed by the call; word 4:
- * a sticky error word the caller zeroes once -- nonzero after a barrier timeout).  dtype bf16 or fp16 (code 2);
- * H * 64 == d, d and ffn multiples of 256.  TW_EUNSUPPORTED when the workgroups cannot all be resident. */
-int tw_decoder_layers(const void* layers, int L, void* x, void* qkv, void* o, void* q, void* h, float* part, int B,
-                      int d, int H, int ffn, int T_max, int Tk, const int* t_dev, float eps, float scale,
-                      unsigned* sync, int dtype, tw_stream_t stream);
 
 /* ---- fp32 arithmetic path (mixed_precision = "no", run_distillation.py:815-823: the reference's default
  * --dtype float32; the fp32 greedy decode pinned token-for-token to HF fp32 generate).  Exact-fp32 MFMA
@@ -266,7 +247,7 @@ int tw_gelu_bwd_f32(const float* g, const float* pre, float* out, int64_t n, tw_
  * tw_gemm_f16: tw_gemm_bf16 for fp16 operands, forward products only (a_trans = b_trans = 0; else 2);
  *   A, B, bias, aux fp16; C and res fp16 (code 2) or fp32; epilogue order as tw_gemm_bf16 with the rounding
  *   to fp16, plus TW_GEMM_CLAMP16: after the residual add, clamp to +-(65504 - 1000) (HF WhisperEncoderLayer,
- *   modeling_whisper.py:409-411, the fp16 encoder stream).  Never routed to hipBLASLt.
+ *   modeling_whisper.py:409-411, the fp16 encoder stream).
  * tw_gemv_f16: tw_gemv_bf16 for fp16 x / W / bias / C (LayerNorm fused as there, fp16 output of the LN).
  * tw_attn_fwd_f16: tw_attn_fwd for fp16 Q/K/V/O (P rounded to fp16 for the PV product, fp32 row sums).
  * tw_mel_to_conv_input_f16: log-mel [B][80][T] fp32 -> fp16 conv1 input [B][T+2][80] (the .to(float16) cast).

@@ -110,29 +110,6 @@ __device__ __forceinline__ void from_f32(bf16& d, float x) { d = f2bf(x); }
 __device__ __forceinline__ void from_f32(f16& d, float x) { d = (_Float16)x; }
 __device__ __forceinline__ void from_f32(float& d, float x) { d = x; }
 
-// Stores of values handed to other workgroups inside one launch (the persistent decoder-step kernel,
-// decode_step.hip): WT = true writes them through to memory -- an agent-scope relaxed atomic store, i.e.
-// global_store_* sc1 -- so the hand-off needs no release fence (no L2 write-back), only the storing waves'
-// drain before the arrival count.  WT = false: a plain store (every other kernel).
-template <bool WT>
-__device__ __forceinline__ void st_wt(bf16* p, bf16 v) {
-  if constexpr (WT)
-    __hip_atomic_store((unsigned short*)p, __builtin_bit_cast(unsigned short, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool WT>
-__device__ __forceinline__ void st_wt(f16* p, f16 v) {
-  if constexpr (WT)
-    __hip_atomic_store((unsigned short*)p, __builtin_bit_cast(unsigned short, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool WT>
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
 template <typename E> __device__ __forceinline__ E e_from_f32(float x) { E d; from_f32(d, x); return d; }
 
 __device__ __forceinline__ float ld_as_f32(const void* p, int dtype, int64_t i) {

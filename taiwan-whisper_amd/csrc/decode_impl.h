@@ -1,5 +1,4 @@
-// Decode attention bodies (one query row per (clip, head) over a KV cache), shared by the per-launch kernels
-// of decode.hip and the persistent decoder-step kernel (decode_step.hip): one source, identical arithmetic.
+// Decode attention bodies (one query row per (clip, head) over a KV cache) of the kernels in decode.hip.
 #pragma once
 #include "common.h"
 
@@ -25,7 +24,7 @@ struct DecP {
 // The body attends keys [lo, hi).  part == nullptr: normalise and store O.  Otherwise (split over keys,
 // flash-decoding) store the chunk's unnormalised o[64], its max m (log2 domain) and sum l to part[0..65]
 // for decode_attn_combine_kernel.
-template <typename E, bool WT = false>
+template <typename E>
 __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, int lo, int hi, float* part) {
   __shared__ float sc[DA_MAX_TK];
   __shared__ float red[DA_THREADS / 64][64];
@@ -116,13 +115,13 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
       lt += red_l[w];
     }
     if (part) {
-      st_wt<WT>(part + tid, acc);
+      part[tid] = acc;
       if (tid == 0) {
-        st_wt<WT>(part + 64, m);
-        st_wt<WT>(part + 65, lt);
+        part[64] = m;
+        part[65] = lt;
       }
     } else {
-      st_wt<WT>((E*)p.o + b * p.sob + h * 64 + tid, e_from_f32<E>(acc / lt));
+      ((E*)p.o)[b * p.sob + h * 64 + tid] = e_from_f32<E>(acc / lt);
     }
   }
 }
@@ -131,7 +130,7 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
 // by the 64 lanes of one wave (lane = output dimension).  Lane c loads chunk c's (m, l) and every lane its
 // column of all chunks up front (independent loads instead of a dependent chain), weights by shuffles.
 constexpr int DA_MAX_CHUNK = 16;
-template <typename E, bool WT = false>
+template <typename E>
 __device__ __forceinline__ void combine_row(const DecP& p, int bh, int nchunk, const float* part) {
   const int lane = threadIdx.x & 63;
   const int b = bh / p.H, h = bh % p.H;
@@ -153,7 +152,7 @@ __device__ __forceinline__ void combine_row(const DecP& p, int bh, int nchunk, c
       }
     }
   }
-  st_wt<WT>((E*)p.o + b * p.sob + h * 64 + lane, e_from_f32<E>(acc / lt));
+  ((E*)p.o)[b * p.sob + h * 64 + lane] = e_from_f32<E>(acc / lt);
 }
 
 

@@ -194,6 +194,29 @@ __device__ __forceinline__ void pp_epi_part(const GemmP& p, f32x4 (&acc)[8][4], 
 // prio 1 around each MFMA phase; 1 = the same with static prio 1 for the trailing wave row
 // (waves 4-7), no flips; 2 = diagnostic: every MFMA phase issued twice (wrong results; measures
 // the fixed per-phase cost); 4 = two 32-MFMA phases per K-tile (default: +4-8 % main loop)
+// s_waitcnt vmcnt(A) if `relax` (a wave-uniform scalar) is nonzero, else vmcnt(B).  The choice is a scalar branch
+// INSIDE the asm block, so the compiler sees straight-line code (a C++ branch here split the persistent kernel's
+// loop body and spilled it: 32 B of scratch per lane).
+template <int A, int B>
+__device__ __forceinline__ void wait_vm_sel(int relax) {
+  static_assert(A >= 0 && A < 64 && B >= 0 && B < 64, "vmcnt immediate");
+  asm volatile("s_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n\ts_waitcnt vmcnt(%1)\n\ts_branch 2f\n"
+               "1:\n\ts_waitcnt vmcnt(%2)\n2:" :: "s"(__builtin_amdgcn_readfirstlane(relax)), "n"(A), "n"(B)
+               : "memory", "scc");
+}
+
+// Store instructions (per lane) of the fast full-tile epilogue of a 256x256 tile (epilogue_fast, 8 fragment rows x
+// 4 fragment columns per wave): one 16-B store per fragment pair of a bf16 output, one per fragment of an fp32
+// output or of the GELU pre-activation side output.  The counted waits of the next tile's first K-tile pair leave
+// these stores in flight: they are younger than every LDS-DMA those waits are for, and s_waitcnt vmcnt counts loads,
+// stores and LDS-DMA together in issue order (MI355X_MICROARCH.md), so waiting for vmcnt(n + stores) completes the
+// same DMA as vmcnt(n) did before the stores -- without also waiting for the stores to be acknowledged.
+template <int KIND>
+constexpr int pp_epi_stores() {
+  return (KIND == EPI_STORE_BF16 || KIND == EPI_GELU || KIND == EPI_RES_BF16) ? 16
+       : (KIND == EPI_STORE_F32 || KIND == EPI_GELU_AUX || KIND == EPI_RES_F32) ? 32 : 0;
+}
+
 template <bool H, int PRIO, int KIND = -1>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   // + 2 x 1 KiB: the bias slice of the current tile (by tile parity), for the fast epilogue (one array:
@@ -208,6 +231,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const int total = my_tiles * nke;                       // K-tiles this workgroup consumes
 
   int si = 0;                                // current tile of this workgroup
+  constexpr int EPS = pp_epi_stores<KIND>();
+  int ep = 0;                                // 1: the previous pair ended with a fast epilogue's EPS stores
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -340,7 +365,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       // segment the A1 staged one segment-pair ago (6 DMA staged since), at a Y segment the
       // A0/B0/B1 staged one pair ago (2 since) — each published by the barriers before its
       // readers' segments.
-      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // PRIO 7: diagnostic, no waits
+      if constexpr (PRIO != 7) {                                 // PRIO 7: diagnostic, no waits
+        if constexpr (EPS > 0) wait_vm_sel<6 + EPS, 6>(ep);
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
       rdA(0, 0); rdB2(0); stg(cpa, cpb, cr, cc, ck, kt + 1, 1, 1);
       // a tile's first K-tile pair: wave 0 stages its 256 bias words (LDS-DMA, no registers).  The next-but-one
       // counted wait of wave 0 covers it and a barrier follows, long before the tile's epilogue reads it;
@@ -354,7 +382,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
         }
       }
       mma2(0);
-      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if constexpr (PRIO != 7) {
+        if constexpr (EPS > 0) wait_vm_sel<2 + EPS, 2>(ep);
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      ep = 0;
       if constexpr (PRIO == 4 || PRIO == 3) rdA(0, 1);      // PRIO 5: diagnostic, A-half 1 not read (LDS-read cost)
       stg(npa, npb, nr, nc, nkl, k2, 0, 0); stg(npa, npb, nr, nc, nkl, k2, 0, 2); stg(npa, npb, nr, nc, nkl, k2, 0, 3);
       mma2(1);
@@ -381,6 +413,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
     }
     if (last) {                                                 // tile finished
       pp_epi_part<H, KIND, 0, 8>(p, acc, si, wm, wn, lane, (const bf16*)(smem + 8 * PP_REGION + (si & 1) * 1024));
+      // the fast epilogue ran (the fp16 kernel runs full tiles only; bf16 ragged tiles take the generic one,
+      // whose store count varies: no relaxed wait after those; cr / cc = rows / columns left from the tile's
+      // corner) and stored (4096: diagnostic, no stores)
+      if constexpr (EPS > 0) ep = (!(p.flags & 4096) && (H || (cr >= 256 && cc >= 256))) ? 1 : 0;
       ++si;
     }
     cpa = npa; cpb = npb; cr = nr; cc = nc; ck = nkl;
@@ -525,8 +561,7 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(GemmP p, int S) {
   }
 }
 
-// GEMV for the batch <= 8 decode step: the body (LN staging, column dots, epilogue) lives in gemv_impl.h,
-// shared with the persistent decoder-step kernel (decode_step.hip)
+// GEMV for the batch <= 8 decode step: the body (LN staging, column dots, epilogue) lives in gemv_impl.h
 template <bool H, int MR, int CPW, int PRE>
 __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                    float eps, GemvKV kv) {
@@ -820,28 +855,8 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
 
 }  // namespace
 
-int tw_vendor_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int b_trans, void* C, int64_t ldc, int M,
-                        int N, int K, const void* bias, void* ws, size_t ws_bytes, hipStream_t stream);
-
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
 void* tw_device_workspace(hipStream_t stream, size_t bytes) { return splitk_workspace(stream, bytes); }
-
-// Which implementation tw_gemm_bf16 runs for a call of this shape: 0 = the hand-written kernels of this file
-// (every call, by default: BASELINE north_star "no dual backends"), 1 = hipBLASLt, only with TW_GEMM_VENDOR=1 (A/B
-// runs against the vendor library: plain forward projections -- K-major operands, bf16 output, bias/round only,
-// alpha 1, K <= 2048, M >= 4096, N >= 256, no forced tile -- and the MN-major-B backward dX products, K <= 8192).
-extern "C" int tw_gemm_backend(int M, int N, int K, int a_trans, int b_trans, int c_dtype, int batch, float alpha,
-                               int flags) {
-  static const int env_vendor = [] {
-    const char* e = getenv("TW_GEMM_VENDOR");
-    return e ? atoi(e) : 0;
-  }();
-  // MN-major B (the dX = dY . W products of the backward) up to K = 8192: hipBLASLt's NN kernels measured
-  // 13-30 % faster than the 128x128 kernel (tools/bench_head_bwd.py VENDOR_NN=1)
-  return (env_vendor && !a_trans && batch == 1 && c_dtype == TW_BF16 && alpha == 1.f &&
-          (flags & 0xff & ~(F_BIAS | F_ROUND)) == 0 && K <= (b_trans ? 8192 : 2048) && M >= 4096 && N >= 256 &&
-          !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) ? 1 : 0;
-}
 
 namespace {
 
@@ -970,17 +985,6 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
                          (flags & F_ACCUM) ? 1 : 0);
       TW_CHECK_LAUNCH();
       return TW_OK;
-    }
-  }
-  // plain forward projections (bias + bf16 out, K <= 2048, M >= 4096): hipBLASLt (csrc/gemm_vendor.hip)
-  if (!H && tw_gemm_backend(M, N, K, a_trans, b_trans, c_dtype, batch, alpha, flags) == 1) {
-    const size_t ws_bytes = (size_t)64 << 20;
-    void* ws = splitk_workspace(stream, ws_bytes);
-    if (ws) {
-      const int r = tw_vendor_gemm_bf16(A, lda, B, ldb, b_trans, C, ldc, M, N, K, (flags & F_BIAS) ? bias : nullptr,
-                                        ws, ws_bytes, stream);
-      if (r == 1) return TW_OK;
-      if (r < 0) return TW_EHIP;
     }
   }
   // mid-sized forward grids (1-4 rounds of 256-tiles): whole rounds persistent + a split-K tail

@@ -1,17 +1,12 @@
-// The GEMM epilogue value and the batch <= 8 GEMV body, shared by gemv_kernel (gemm.hip, one launch per
-// LN + Linear of the decode step) and the persistent decoder-step kernel (decode_step.hip, every Linear of
-// every decoder layer in one launch).  One source for both, so the two paths are bit-identical by
-// construction: the same LN statistics and order, the same per-lane k order of the fp32 FMAs, the same
-// butterfly sum and epilogue.
+// The GEMM epilogue value (also the skinny / split-K reduce kernels' per-element epilogue) and the batch <= 8
+// GEMV body of gemv_kernel (gemm.hip, one launch per LN + Linear of the decode step).
 #pragma once
 #include "gemm_impl.h"
 
 namespace twg {
 
 // the epilogue value of C[m][n] (writes the GELU pre-activation to aux on the way), before the store
-// WT (the persistent decoder-step kernel): the residual operand was written by other workgroups of the launch:
-// read it with a vector load that misses every cache (an agent-scope relaxed atomic load), never the scalar path
-template <bool H, bool WT = false>
+template <bool H>
 __device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v) {
   const int flags = p.flags;
   v *= p.alpha;
@@ -25,14 +20,7 @@ __device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v
   if (flags & F_RES) {
     const int mr = p.res_mod > 0 ? (m % p.res_mod) : m;
     const int64_t ri = (int64_t)mr * p.ldr + n;
-    if constexpr (WT) {
-      v += p.res_dtype == TW_BF16
-               ? e2f<H>(__builtin_bit_cast(bf16, __hip_atomic_load((const unsigned short*)p.res + ri, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT)))
-               : __hip_atomic_load((const float*)p.res + ri, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      v += ld16_as_f32<H>(p.res, p.res_dtype, ri);
-    }
+    v += ld16_as_f32<H>(p.res, p.res_dtype, ri);
   }
   if (flags & F_ACCUM) v += ld16_as_f32<H>(p.C, p.c_dtype, (int64_t)m * p.ldc + n);
   if (flags & F_CLAMP16) v = clamp_f16_stream(rnd<H>(v));
@@ -129,7 +117,7 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 }
 
 // columns n0 .. n0 + CPW - 1 against the staged rows (xs visible to this wave), then the epilogue by lane 0
-template <bool H, int MR, int CPW, int PRE, bool WT = false>
+template <bool H, int MR, int CPW, int PRE>
 __device__ __forceinline__ void gemv_finish(const GemmP& p, const GemvKV& kv, const bf16* xs, int n0, int lane,
                                             const bf16x8 (&wpre)[CPW][PRE]) {
   const int K = p.K;
@@ -178,14 +166,14 @@ __device__ __forceinline__ void gemv_finish(const GemmP& p, const GemvKV& kv, co
       for (int r = 0; r < MR; ++r) {
         const int n = n0 + c;
         if (r < p.M && n < p.N) {
-          const float v = epi_value<H, WT>(p, r, n, acc[c][r]);
+          const float v = epi_value<H>(p, r, n, acc[c][r]);
           const int64_t co = (int64_t)r * p.ldc + n;
-          if (p.c_dtype == TW_BF16) st_wt<WT>((bf16*)p.C + co, f2e<H>(v));
-          else st_wt<WT>((float*)p.C + co, v);
+          if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
+          else ((float*)p.C)[co] = v;
           if (kv.cache && n >= kv.col0) {
             const int64_t ko = r * kv.sb + t * kv.ld + (n - kv.col0);
-            if (p.c_dtype == TW_BF16) st_wt<WT>((bf16*)kv.cache + ko, f2e<H>(v));
-            else st_wt<WT>((float*)kv.cache + ko, v);
+            if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2e<H>(v);
+            else ((float*)kv.cache)[ko] = v;
           }
         }
       }

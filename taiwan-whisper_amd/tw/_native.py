@@ -16,7 +16,6 @@ P, I64, I32, F32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 
 # name -> argtypes (return type is always int status)
 SIGNATURES = {
-    "tw_gemm_backend": [I32, I32, I32, I32, I32, I32, I32, F32, I32],
     "tw_gemm_bf16": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I32, I64, I64, I64, F32, P,
                      P, I64, I64, I32, I32, P, I64, I64, I32, P],
     "tw_flac_info": [P, I64, P],
@@ -56,7 +55,6 @@ SIGNATURES = {
     "tw_kv_append": [P, I64, P, I64, I64, I32, I32, I32, P, P],
     "tw_kv_head_major": [P, I64, P, I32, I32, I32, I32, P],
     "tw_step_advance": [P, I32, P],
-    "tw_decoder_layers": [P, I32, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, P, F32, F32, P, I32, P],
     # fp16 arithmetic path (torch_dtype=float16 decode: run_eval.py:99, run_pseudo_labelling.py:461-463)
     "tw_gemm_f16": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I32, I64, I64, I64, F32, P,
                     P, I64, I64, I32, I32, P, I64, I64, I32, P],
@@ -93,11 +91,6 @@ def lib():
             f.restype = ctypes.c_int
         _lib = l
     return _lib
-
-
-def query(name: str, *args) -> int:
-    """A C-ABI entry whose int return is a value, not a status (tw_gemm_backend)."""
-    return int(getattr(lib(), name)(*args))
 
 
 def call(name: str, *args):

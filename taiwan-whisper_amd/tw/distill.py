@@ -107,6 +107,7 @@ class DistillationTrainer:
         if self.overlap_update and not freeze_encoder:
             raise ValueError("overlap_update needs a frozen encoder: the next forward must read no trainable weight")
         self._update = None      # (lr, t) of a launched, not yet applied update
+        self.exchange_events = None   # list -> (start, end) events around each exchange wait (bench.py)
         set_trainable_like_reference(student, freeze_encoder, freeze_decoder, freeze_embed_positions)
         self.train_encoder = not freeze_encoder
         self.freeze_encoder, self.freeze_decoder = freeze_encoder, freeze_decoder
@@ -256,9 +257,19 @@ class DistillationTrainer:
         self.bw.on_ready = None
 
     def wait_grad_exchange(self):
-        """The compute stream waits for every launched bucket (a stream dependency under RCCL)."""
-        for w in getattr(self, "_pending", []):
+        """The compute stream waits for every launched bucket (a stream dependency under RCCL).  With
+        `exchange_events` a list (bench.py), an event pair brackets the wait on the compute stream: their
+        distance is the exchange time the step leaves exposed."""
+        pend = getattr(self, "_pending", [])
+        ev = getattr(self, "exchange_events", None) if pend else None
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        for w in pend:
             w.wait()
+        if ev is not None:
+            e1.record()
+            ev.append((e0, e1))
         self._pending, self._reduced = [], []
 
     def all_reduce_grads(self):

@@ -31,11 +31,6 @@ import torch
 from . import ops as F
 
 _XKV_HEAD_MAJOR = os.environ.get("TW_XKV_HEAD_MAJOR", "1") != "0"
-# batch <= 8: every decoder layer of a step in one persistent launch (tw_decoder_layers, csrc/decode_step.hip),
-# opt-in with TW_DECODE_MEGA=1: bit-identical to the per-launch step (tests/test_decode_step_gpu.py) but measured
-# slower on c5 (1.79 vs 1.08 ms per decode step, profiles/r03_v1_c5_*.log): a grid barrier + its acquire cost more
-# than the graph-replayed kernel boundary it replaces
-MEGA = os.environ.get("TW_DECODE_MEGA", "0") == "1"
 
 
 class DecodeSession:
@@ -79,11 +74,6 @@ class DecodeSession:
         # separate LayerNorm
         self.gemv = B <= 8 and model.compute in ("bf16", "fp16") and d % 256 == 0
         self.gemv_ln = self.gemv and model.stream_dtype == act
-        # the persistent decoder-step kernel takes the same operands as the GEMV path (16-bit stream, LN fused,
-        # head-major cross K/V); a per-layer pointer table, the cross-attention partials and the barrier words
-        self.mega = MEGA and self.gemv_ln and self.hm and cfg.decoder_ffn_dim % 256 == 0
-        if self.mega:
-            self._build_layer_table()
 
     def set_encoder(self, enc16):
         """(Re)project the cross-attention K/V of every decoder layer in place (graph-safe).  enc16 holds B*Tk
@@ -113,34 +103,6 @@ class DecodeSession:
             else:
                 m._lin(enc16, wkv, bkv, kv)
         del proj
-
-    def _build_layer_table(self):
-        m, B, d, H, Tk = self.m, self.B, self.d, self.H, self.Tk
-        rows = []
-        for i in range(m.config.decoder_layers):
-            p = f"model.decoder.layers.{i}"
-            kv = self.cross_kv[i]
-            hv = B * H * Tk * 64
-            ts = [m.ln_param(p + ".self_attn_layer_norm.weight"), m.ln_param(p + ".self_attn_layer_norm.bias"),
-                  m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d)),
-                  m.wspan(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", (3 * d,)),
-                  m._w16(p + ".self_attn.out_proj.weight"), m._w16(p + ".self_attn.out_proj.bias"),
-                  m.ln_param(p + ".encoder_attn_layer_norm.weight"), m.ln_param(p + ".encoder_attn_layer_norm.bias"),
-                  m._w16(p + ".encoder_attn.q_proj.weight"), m._w16(p + ".encoder_attn.q_proj.bias"),
-                  kv, kv[hv:],
-                  m._w16(p + ".encoder_attn.out_proj.weight"), m._w16(p + ".encoder_attn.out_proj.bias"),
-                  m.ln_param(p + ".final_layer_norm.weight"), m.ln_param(p + ".final_layer_norm.bias"),
-                  m._w16(p + ".fc1.weight"), m._w16(p + ".fc1.bias"), m._w16(p + ".fc2.weight"),
-                  m._w16(p + ".fc2.bias"), self.self_kv[i]]
-            rows.append([t.data_ptr() for t in ts])
-        self._ltab = torch.tensor(rows, dtype=torch.int64).view(-1).to(m.device)
-        self._part = torch.empty(B * H * ((Tk + 127) // 128) * 66, dtype=torch.float32, device=m.device)
-        self._sync = torch.zeros(8, dtype=torch.int32, device=m.device)
-
-    def check(self):
-        """Raise if a persistent decoder-step launch gave up at a grid barrier (its sticky error word)."""
-        if self.mega and int(self._sync[4].item()) != 0:
-            raise RuntimeError("tw_decoder_layers: a grid barrier timed out (workgroups not co-resident?)")
 
     def _ln(self, x, name):
         m = self.m
@@ -180,10 +142,7 @@ class DecodeSession:
         x, o, t_dev = self.x, self.o, self.t_dev
         F.embed_step(self.cur, E, Pe, x, t_dev, T_max)
         sb = T_max * 2 * d
-        if self.mega:
-            F.decoder_layers(self._ltab, m.config.decoder_layers, x, self.qkv, o, self.q, self.h, self._part, B, d, H,
-                             m.config.decoder_ffn_dim, T_max, self.Tk, t_dev, 1e-5, 0.125, self._sync)
-        for i in range(0 if self.mega else m.config.decoder_layers):
+        for i in range(m.config.decoder_layers):
             p = f"model.decoder.layers.{i}"
             # self attention: fused QKV -> staging; k, v appended at row t of the cache
             wqkv = m.wspan(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", (3 * d, d))
@@ -359,7 +318,6 @@ class _Decoder:
             t += 1
             if (t - P) % 8 == 7 and bool(sel.done.all()):
                 break
-        sess.check()
         gen = sel.ids[:, P:t + 1]
         # trim trailing columns in which every row had already finished (HF stops at the step
         # where the last row emits eos)
@@ -455,6 +413,20 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     if kw.get("_keep") is not None:          # tests: the decoder (and its device caches) outlive the call
         kw["_keep"].append(dec)
     return dec.run(enc16, prompt.to(model.device))
+
+
+def batch_rows_independent(model):
+    """True where each row of a decode batch of <= 8 rows is bit-identical to its batch-1 decode: on the 16-bit
+    compute paths every decode-step Linear is a per-row GEMV (d % 256 == 0) or the skinny GEMM, whose K order per
+    output does not depend on the batch (no split-K at <= 32 rows); tests/test_fallback_gpu.py runs the skinny
+    form (micro, d = 128).  The fp32 path's GEMMs are not shown row-independent, so it decodes one at a time."""
+    return model.compute in ("bf16", "fp16")
+
+
+def row_tokens(raw, eos):
+    """One row of a decoded batch as its own batch-1 decode returns it: up to and including its first eos."""
+    raw = list(raw)
+    return raw[:raw.index(eos) + 1] if eos in raw else raw
 
 
 def compression_ratio(tokens, vocab_size):
@@ -565,7 +537,9 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
             seeds = [(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1) for fi in range(len(temps))]
             attempts = [(0, dec, enc16, ptens, [temps[0] or 0.0], [seeds[0]])]
             rest = list(range(1, len(temps)))
-            per = 8 if fallback_batch else 1                 # fallback_batch=False: one attempt at a time (A/B, tests)
+            # fallback_batch=False: one attempt at a time (A/B, tests); so does the fp32 compute path, whose rows are
+            # not shown independent of the batch (batch_rows_independent)
+            per = 8 if fallback_batch and batch_rows_independent(model) else 1
             for fb in range(0, len(rest), per):
                 grp = rest[fb:fb + per]
                 attempts.append((grp[0], None, None, None, [temps[f] or 0.0 for f in grp], [seeds[f] for f in grp]))
@@ -577,6 +551,9 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                     p_ = ptens.repeat(nb, 1)
                 raws = d_.run(e_, p_, temperature=tl if len(tl) > 1 else tl[0], seed=sl if len(sl) > 1 else sl[0],
                               no_speech=ns).tolist()
+                # a batch is cut at its LAST row's first eos, so a row that finished earlier carries extra eos (=pad)
+                # columns; each row is cut at its own first eos, which is exactly what its batch-1 decode returns
+                raws = [row_tokens(r, eos) for r in raws]
                 done_here = False
                 for r, raw in enumerate(raws):
                     fi, temp = fi0 + r, temps[fi0 + r]

@@ -452,8 +452,8 @@ class WhisperForConditionalGeneration:
         """Whether the stream-updating Linear of a `kind` block ("attn" = out_proj, "mlp" = fc2) writes its bf16
         output and leaves the residual add to the next LayerNorm (tw_add_layernorm_fwd, the same add): on the
         student's fp32 stream for both (the fp32 read-modify-write leaves the persistent GEMM's epilogue), on
-        the bf16 teacher stream for out_proj only (the plain projection then runs on hipBLASLt; at fc2 the extra
-        LN traffic costs what the epilogue saves).  DESIGN.md §5; TW_DEFER_RES=0 disables (A/B runs)."""
+        the bf16 teacher stream for out_proj only (the plain-bias projection then runs the store-only epilogue; at
+        fc2 the extra LN traffic costs what the epilogue saves).  DESIGN.md §5; TW_DEFER_RES=0 disables (A/B runs)."""
         # tw_add_layernorm_fwd: D % 256 == 0 and D <= 1280 (every Whisper size), else the residual epilogue
         if _DEFER_RES == "0" or self.act_dtype != torch.bfloat16 or self.config.d_model % 256 or self.config.d_model > 1280:
             return False

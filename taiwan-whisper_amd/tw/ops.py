@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from ._native import call, query
+from ._native import call
 from .profiling import KernelTimer
 
 F32, BF16, F16 = 0, 1, 2
@@ -85,9 +85,6 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
         assert aux.dtype == h
         _need(aux, (batch - 1) * sAux + (M - 1) * ldaux + N, "gemm aux")
     fam = "gemm_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
-    if KernelTimer.active is not None and query("tw_gemm_backend", M, N, K, int(a_trans), int(b_trans), _dt(C),
-                                                 batch, float(alpha), flags) == 1:
-        fam += "_lt"                 # timed apart: this call runs on hipBLASLt (include/tw_hip.h tw_gemm_backend)
     flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
     KernelTimer.wrap(fam, flops, lambda: call(
         "tw_gemm_f16" if h == torch.float16 else "tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
@@ -514,25 +511,6 @@ def kv_head_major(src, ld, dst, B, Tk, H):
     _need(src, (B * Tk - 1) * ld + 2 * 64 * H, "kv_head_major src")
     _need(dst, 2 * B * H * Tk * 64, "kv_head_major dst")
     call("tw_kv_head_major", src.data_ptr(), ld, dst.data_ptr(), B, Tk, H, _dt(src), _stream())
-
-
-def decoder_layers(table, L, x, qkv, o, q, h, part, B, d, H, ffn, T_max, Tk, t_dev, eps, scale, sync):
-    """tw_decoder_layers: every decoder layer of one greedy step (B <= 8) in one persistent launch
-    (include/tw_hip.h).  table: int64 [L * 21] device pointers (see the header for their order)."""
-    dt = x.dtype
-    assert dt in HALF and all(t.dtype == dt for t in (qkv, o, q, h)), "decoder_layers: 16-bit buffers"
-    assert table.dtype == torch.int64 and table.is_cuda and table.numel() == L * 21
-    assert part.dtype == torch.float32 and sync.dtype == torch.int32 and sync.numel() >= 8
-    assert t_dev.dtype == torch.int32 and 1 <= B <= 8 and H * 64 == d
-    _need(x, B * d, "decoder_layers x")
-    _need(qkv, B * 3 * d, "decoder_layers qkv")
-    _need(o, B * d, "decoder_layers o")
-    _need(q, B * d, "decoder_layers q")
-    _need(h, B * ffn, "decoder_layers h")
-    _need(part, B * H * ((Tk + 127) // 128) * 66, "decoder_layers part")
-    call("tw_decoder_layers", table.data_ptr(), L, x.data_ptr(), qkv.data_ptr(), o.data_ptr(), q.data_ptr(),
-         h.data_ptr(), part.data_ptr(), B, d, H, ffn, T_max, Tk, t_dev.data_ptr(), float(eps), float(scale),
-         sync.data_ptr(), _dt(x), _stream())
 
 
 def step_advance(t_dev, by=1):

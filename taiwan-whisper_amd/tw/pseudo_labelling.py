@@ -127,8 +127,8 @@ def transcribe_files(paths: Sequence[str], transcribe: Callable[[Sequence[np.nda
     bounded number of decoded waveforms whatever the manifest size; chunks of consecutive files fill
     batches of `batch_size` across file boundaries.  `on_done(path, rows)` runs as soon as a file's last
     chunk is transcribed (the reference writes each CSV when its file finishes, initial_inference.py:106-
-    115).  A batch whose transcription or text decoding raises marks every file with a chunk in it as
-    failed (logged, result None, its other chunks dropped) and the run goes on (:116-119)."""
+    115).  A batch whose transcription or text decoding raises is retried one file at a time; a file whose own
+    chunks raise is failed (logged, result None, its other chunks dropped) and the run goes on (:116-119)."""
     results: Dict[str, Optional[List[dict]]] = {}
     pending: List[Tuple[str, float, float, np.ndarray]] = []
     counts: Dict[str, int] = {}
@@ -139,23 +139,41 @@ def transcribe_files(paths: Sequence[str], transcribe: Callable[[Sequence[np.nda
         if on_done is not None and r is not None:
             on_done(p, r)
 
+    def fail(bad, e):
+        for p in bad:
+            log(f"Failed to transcribe {p}, error: {e}")
+            rows.pop(p, None)
+            counts.pop(p, None)
+            results[p] = None
+        pending[:] = [c for c in pending if c[0] not in set(bad)]
+
+    def run(batch):
+        toks = transcribe([c[3] for c in batch])
+        return [decode(t) for t in toks]
+
     def flush(force=False):
         while pending and (force or len(pending) >= batch_size):
             batch = pending[:batch_size]
             del pending[:batch_size]
+            files = list(dict.fromkeys(c[0] for c in batch))
             try:
-                toks = transcribe([c[3] for c in batch])
-                texts = [decode(t) for t in toks]
-            except Exception as e:              # noqa: BLE001 -- log the files of the batch and go on
-                bad = list(dict.fromkeys(c[0] for c in batch))
-                for p in bad:
-                    log(f"Failed to transcribe {p}, error: {e}")
-                    rows.pop(p, None)
-                    counts.pop(p, None)
-                    results[p] = None
-                pending[:] = [c for c in pending if c[0] not in set(bad)]
-                continue
-            for (p, s, e, _), t in zip(batch, texts):
+                done = list(zip(batch, run(batch)))
+            except Exception as e:              # noqa: BLE001 -- log the failing files and go on
+                if len(files) == 1:
+                    fail(files, e)
+                    continue
+                # chunks of several files share the batch: retry it one file at a time, so only a file whose own
+                # chunks raise is failed (the reference fails only the file that raised, :106-119)
+                done = []
+                for p in files:
+                    sub = [c for c in batch if c[0] == p]
+                    try:
+                        done.extend(zip(sub, run(sub)))
+                    except Exception as e1:     # noqa: BLE001
+                        fail([p], e1)
+            for (p, s, e, _), t in done:
+                if p not in rows:               # failed in an earlier batch
+                    continue
                 rows[p].append({"start": f"{s:.2f}", "end": f"{e:.2f}", "text": t})
                 if len(rows[p]) == counts[p]:
                     counts.pop(p)

@@ -16,6 +16,8 @@ What produces each vector:
     and `mix_language_embeddings` (`utils/model_utils.py:4-14`)         -> student.npz
   * HF `generate(num_beams=1)` greedy with forced prompt                 -> greedy.npz
   * the same forward / greedy / timestamp / long-form runs with torch_dtype=float16 -> fp16.npz
+  * HF generate at the real large-v2 dims (fp32 and float16): greedy, timestamps, long-form gates
+                                                                         -> lv2_decode.npz
 
 Only small slices / checksums are stored (fixtures are data, no reference source).
 """
@@ -377,6 +379,96 @@ def gen_fp16(out):
     out["f16_fb_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
 
 
+class _MarginSpy:
+    """A logits processor appended after HF's own (generate merges a custom processor list after the built-in
+    ones): records, per decode step and row, the gap between the two largest PROCESSED scores -- how close the
+    greedy choice was to a tie."""
+
+    def __init__(self):
+        self.steps = []
+
+    def __call__(self, input_ids, scores):
+        top = scores.float().topk(2, dim=-1).values
+        self.steps.append((top[:, 0] - top[:, 1]).numpy().astype(np.float32))
+        return scores
+
+
+LV2_SEED = 61
+
+
+def lv2_features():
+    """Two 30 s synthetic clips (the bench's sine + noise recipe) and a 45 s long-form input (the first 4 500 frames
+    of longform_features' deterministic draw)."""
+    short = logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(3, 14.0)])
+    return short, longform_features()[:, :, :4500]
+
+
+def gen_lv2_decode(out):
+    """HF generate at the REAL large-v2 dimensions (d 1280, 32 + 32 layers, 20 heads) -- the model of BASELINE c4 / c5
+    -- with documented random weights (oracle/weights.make_weights(large-v2, LV2_SEED, per_tensor=True,
+    embed_std=0.05)), in fp32 and with torch_dtype=float16 (run_eval.py:99, run_pseudo_labelling.py:461-463):
+      {f32,f16}_greedy_ids / _margin : greedy, 2 clips, [SOT, zh, transcribe, notimestamps], 48 new tokens
+                                       (run_pseudo_labelling.py:917-922 without timestamps)
+      {f32,f16}_ts_ids / _margin     : return_timestamps=True, language zh, 48 new tokens
+      f32_long_ids, f32_long_avg_logprobs, f32_long_ns_probs : 45 s long-form (2 windows), temperature (0.0,),
+                                       thresholds that never fire, per-window gates (run_eval.py:659-665 path)
+    _margin = per step and row, the top-1 minus top-2 processed score (_MarginSpy)."""
+    from transformers import GenerationConfig
+    from transformers.generation.logits_process import LogitsProcessorList
+    cfg = CONFIGS["large-v2"]
+    w = make_weights(cfg, LV2_SEED, per_tensor=True, embed_std=0.05)
+    short, lf = lv2_features()
+    prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
+    for dt, tag in ((torch.float32, "f32"), (torch.float16, "f16")):
+        m = hf_model(cfg, w, dt).eval()
+        feats = torch.from_numpy(short).to(dt)
+        m.generation_config = GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
+                                               pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
+                                               begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=448,
+                                               num_beams=1, do_sample=False,
+                                               no_timestamps_token_id=SPECIAL["notimestamps"])
+        spy = _MarginSpy()
+        with torch.no_grad():
+            out[f"{tag}_greedy_ids"] = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * 2), max_new_tokens=48,
+                                                  logits_processor=LogitsProcessorList([spy])).numpy()
+        out[f"{tag}_greedy_margin"] = np.stack(spy.steps)
+        m.generation_config = ts_generation_config()
+        spy = _MarginSpy()
+        with torch.no_grad():
+            out[f"{tag}_ts_ids"] = m.generate(feats, return_timestamps=True, language="zh", task="transcribe",
+                                              max_new_tokens=48, logits_processor=LogitsProcessorList([spy])).numpy()
+        out[f"{tag}_ts_margin"] = np.stack(spy.steps)
+        if tag == "f32":
+            lt = torch.from_numpy(lf)
+            kw = dict(attention_mask=torch.ones(1, lt.shape[-1], dtype=torch.long), return_timestamps=True,
+                      language="zh", task="transcribe")
+            rec = {"avg": [], "ns": []}
+            orig_need = type(m)._need_fallback
+
+            def need_spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
+                         temperature):
+                rec["avg"].append(float(self._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence,
+                                                                    temperature)))
+                from transformers.generation.logits_process import WhisperNoSpeechDetection
+                for p_ in logits_processor or []:
+                    if isinstance(p_, WhisperNoSpeechDetection):
+                        rec["ns"].append(float(p_.no_speech_prob[index]))
+                return orig_need(self, seek_sequence, seek_outputs, index, logits_processor, generation_config,
+                                 vocab_size, temperature)
+            type(m)._need_fallback = need_spy
+            try:
+                with torch.no_grad():
+                    out["f32_long_ids"] = m.generate(lt, temperature=(0.0,), logprob_threshold=-1e9,
+                                                     no_speech_threshold=1.0, **kw).numpy()
+            finally:
+                type(m)._need_fallback = orig_need
+            out["f32_long_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
+            out["f32_long_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
+        del m
+    out["prompt"] = np.array(prompt)
+    out["seed"] = np.int64(LV2_SEED)
+
+
 # ------------------------------------------------------------------------------------------------
 # BASELINE-config parity fixtures (c1 / c2 / c3 dims).  The reference path is HF Whisper under
 # bf16 autocast (run_distillation.py:815-830 mixed_precision="bf16"; accelerate wraps every prepared
@@ -399,8 +491,8 @@ CFG_CASES = {
     # frozen shared encoder, a <|startofprev|> prompt (A7 teacher-input quirk at full size)
     "c3": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=1, freeze_encoder=True,
                freeze_embed_positions=True, label_seed=43, secs=[30.0], prompt=True),
-    # c3 at B = 10: encoder rows 15 000 and decoder rows 4 470 (>= 4096), so the projections take the production
-    # route of the B = 64 step (tw_gemm_backend: hipBLASLt for the plain bias projections)
+    # c3 at B = 10: encoder rows 15 000 and decoder rows 4 470, the encoder projections on the persistent kernel of
+    # the B = 64 step
     "c3b10": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=10, freeze_encoder=True,
                   freeze_embed_positions=True, label_seed=45, secs=[30.0, 27.5, 12.0, 30.0, 8.0, 19.0, 30.0, 24.0,
                                                                     30.0, 15.5], prompt=True),
@@ -516,6 +608,7 @@ def main():
     only = sys.argv[1:]
     for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
+                     ("lv2_decode", gen_lv2_decode),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
                      ("cfg_c3", lambda o: gen_cfg("c3", o)), ("cfg_c3b10", lambda o: gen_cfg("c3b10", o))):
         if only and name not in only:

@@ -1,7 +1,7 @@
 """Distillation-step parity at the BASELINE configs' dimensions (c1 tiny<-tiny, c2 small<-large-v2,
-c3 distil-32-2<-large-v2, and c3 again at B = 10 so that every plain projection takes the route of the B = 64
-bench step: encoder rows 15 000, decoder rows 4 470 >= 4096 -> hipBLASLt per tw_gemm_backend) against the
-reference path itself.
+c3 distil-32-2<-large-v2, and c3 again at B = 10: encoder rows 15 000 and decoder rows 4 470, so the encoder
+projections run on the persistent 256x256 kernel as in the B = 64 bench step and the decoder ones on the 128x128
+kernel) against the reference path itself.
 
 Fixtures: tests/golden/cfg_c{1,2,3}.npz, made by tests/golden/make_golden.py gen_cfg in the build
 container: HF Transformers WhisperForConditionalGeneration running the reference's train_step

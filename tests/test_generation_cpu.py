@@ -1,0 +1,102 @@
+"""Host logic of long-form decoding (tw/generation.py _longform) with a scripted stand-in for the device decoder:
+the speculative fallback batch must give what decoding the attempts one at a time gives (HF
+generate_with_fallback decodes them one by one: generation_whisper.py:970-1090), also when the accepted row of a
+batch finishes before another row of that batch on a window that is not the last one."""
+import types
+
+import pytest
+import torch
+
+from tw import generation
+from tw.config import GenerationConfig
+
+EOS = 50257
+TS0 = 50364            # <|0.00|>
+
+
+class _Sel:
+    def __init__(self, nb):
+        self.sum_logp = torch.zeros(nb)
+
+
+class _ScriptedDecoder:
+    """Stands in for generation._Decoder: row r of a run decodes SCRIPT[(window, temperature)], and the batch is
+    cut where its longest row emits eos, the rows that finished earlier padded with eos -- what the device
+    decoder returns (DecodeSession ids are eos-filled, _Decoder.run trims at the last row's first eos)."""
+    script = {}
+
+    def __init__(self, model, gc, nb, Tk, P, ml, timestamps, use_graph, track=False):
+        self.nb = nb
+        self.sel = _Sel(nb)
+        self.ns_logp = torch.zeros(nb)
+
+    def run(self, enc16, prompt, temperature=0.0, seed=0, no_speech=None):
+        win = int(enc16.flatten()[0].item())
+        temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
+        assert len(temps) == self.nb
+        rows = [list(self.script[(win, round(t, 1))]) for t in temps]
+        L = max(len(r) for r in rows)
+        for i, r in enumerate(rows):
+            self.sel.sum_logp[i] = -0.1 * len(r)
+        return torch.tensor([r + [EOS] * (L - len(r)) for r in rows], dtype=torch.int64)
+
+
+def _model():
+    cfg = types.SimpleNamespace(max_source_positions=1500, max_target_positions=448, vocab_size=51865, d_model=128)
+    m = types.SimpleNamespace(config=cfg, device=torch.device("cpu"), compute="bf16")
+    m.conv_input = lambda feats: feats
+    m.encode = lambda x: x[:, :1, :1].reshape(1, 1).clone()     # the window id the features carry
+    return m
+
+
+def _run(monkeypatch, fallback_batch, script):
+    monkeypatch.setattr(generation, "_Decoder", _ScriptedDecoder)
+    _ScriptedDecoder.script = script
+    feats = torch.zeros(1, 80, 6000)
+    feats[..., 3000:] = 1.0                                      # window 1 carries id 1
+    gc = GenerationConfig(decoder_start_token_id=50258, eos_token_id=EOS, pad_token_id=EOS,
+                          no_timestamps_token_id=50363, suppress_tokens=[], lang_to_id={"<|zh|>": 50260})
+    trace = []
+    out = generation._longform(_model(), gc, feats, None, "zh", "transcribe", None, 40, False, 3000, trace,
+                               temperature=(0.0, 0.2, 0.4, 0.6), compression_ratio_threshold=1.35,
+                               fallback_batch=fallback_batch)
+    return out[0].tolist(), trace
+
+
+def _script():
+    loop = [TS0] + [100, 101] * 20 + [EOS]                      # compression ratio >> 1.35: falls back
+    short = [TS0, 100, 101, TS0 + 100, EOS]                      # accepted; finishes first in its batch
+    longer = [TS0, 300, 301, 302, 303, 304, 305, 306, 307, TS0 + 150, EOS]
+    last = [TS0, 400, 401, TS0 + 50, EOS]
+    return {(0, 0.0): loop, (0, 0.2): short, (0, 0.4): longer, (0, 0.6): longer, (1, 0.0): last}
+
+
+def test_batched_fallback_row_finishing_first_equals_sequential(monkeypatch):
+    a, ta = _run(monkeypatch, True, _script())
+    b, tb = _run(monkeypatch, False, _script())
+    assert any(t["batch"] > 1 for t in ta) and all(t["batch"] == 1 for t in tb)
+    assert a == b
+    # window 0 accepted at T = 0.2 (its predicted eos cut: not the last window), window 1 at T = 0 (final: eos kept)
+    assert a == [TS0, 100, 101, TS0 + 100, TS0, 400, 401, TS0 + 50, EOS]
+    assert EOS not in a[:-1]
+
+
+def test_row_tokens():
+    assert generation.row_tokens([1, 2, EOS, EOS, EOS], EOS) == [1, 2, EOS]
+    assert generation.row_tokens([1, 2, 3], EOS) == [1, 2, 3]
+    assert generation.row_tokens([EOS, EOS], EOS) == [EOS]
+
+
+@pytest.mark.parametrize("compute,batched", [("bf16", True), ("fp16", True), ("fp32", False)])
+def test_fallback_batch_only_where_rows_are_independent(monkeypatch, compute, batched):
+    monkeypatch.setattr(generation, "_Decoder", _ScriptedDecoder)
+    _ScriptedDecoder.script = _script()
+    m = _model()
+    m.compute = compute
+    feats = torch.zeros(1, 80, 6000)
+    feats[..., 3000:] = 1.0
+    gc = GenerationConfig(eos_token_id=EOS, pad_token_id=EOS, lang_to_id={"<|zh|>": 50260})
+    trace = []
+    generation._longform(m, gc, feats, None, "zh", "transcribe", None, 40, False, 3000, trace,
+                         temperature=(0.0, 0.2, 0.4, 0.6), compression_ratio_threshold=1.35, fallback_batch=True)
+    assert any(t["batch"] > 1 for t in trace) == batched

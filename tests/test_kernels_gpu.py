@@ -353,56 +353,6 @@ def test_gemm_sk_tail_forward(M, N, K):
     assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
 
 
-@pytest.mark.parametrize("M,N,K,has_bias", [(28608, 3840, 1280, True), (8200, 51904, 1280, False),
-                                             (5000, 1288, 1280, True)])
-def test_gemm_vendor_plain_forward(M, N, K, has_bias):
-    """Plain forward projections (bias + bf16 out, K <= 2048, M >= 4096) run on hipBLASLt: the same
-    autocast arithmetic (fp32 accumulate, + bf16 bias, one bf16 round) as the persistent kernel, so
-    the outputs agree within one bf16 ulp (the fp32 sums may differ in order: plus a cancellation term),
-    sampled rows match fp64 within one ulp, and reruns are bit-identical."""
-    from tw import ops
-    g = torch.Generator().manual_seed(M + N + K)
-    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
-    bias = torch.randn(N, generator=g)
-    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
-    kw = dict(bias=bd) if has_bias else {}
-    outs = {}
-    for name, f in (("pp", ops.GEMM_TILE256PP), ("vendor", 0), ("vendor2", 0)):
-        C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
-        ops.gemm(Ad, Wd, C, M, N, K, lda=K, ldb=K, ldc=N, flags=ops.GEMM_ROUND | f, **kw)
-        outs[name] = C
-    torch.cuda.synchronize()
-    got, ref = outs["vendor"].float(), outs["pp"].float()
-    assert not torch.isnan(got).any()
-    assert torch.equal(outs["vendor"], outs["vendor2"])
-    tol = torch.maximum(got.abs(), ref.abs()) * 2 ** -7 + 2e-6 * float(ref.abs().max())
-    assert bool(((got - ref).abs() <= tol).all()), float(((got - ref).abs() - tol).max())
-    rows = torch.tensor([0, M // 3, M - 1])
-    want = bf(A[rows]).double() @ bf(W).double().T + (bf(bias).double() if has_bias else 0)
-    want = bf(want.float()).float()
-    assert (got[rows.to(DEV)].cpu() - want).abs().max() <= 2 ** -7 * want.abs().max()
-
-
-def test_gemm_vendor_mn_major_b():
-    """dX = dY . W products (MN-major B, K <= 8192) also run on hipBLASLt: within one bf16 ulp (+ the
-    cancellation term) of the 128x128 kernel and bit-identical on reruns."""
-    from tw import ops
-    M, N, K = 8192, 1280, 3840
-    g = torch.Generator(device=DEV).manual_seed(11)
-    dy = bf(torch.randn(M, K, device=DEV, generator=g))
-    W = bf(torch.randn(K, N, device=DEV, generator=g) * 0.05)
-    outs = []
-    for f in (ops.GEMM_TILE128, 0, 0):
-        C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
-        ops.gemm(dy, W, C, M, N, K, lda=K, ldb=N, ldc=N, b_trans=True, flags=ops.GEMM_ROUND | f)
-        outs.append(C)
-    torch.cuda.synchronize()
-    ref, got = outs[0].float(), outs[1].float()
-    assert torch.equal(outs[1], outs[2]) and not torch.isnan(got).any()
-    tol = torch.maximum(got.abs(), ref.abs()) * 2 ** -7 + 2e-6 * float(ref.abs().max())
-    assert bool(((got - ref).abs() <= tol).all())
-
-
 def test_transpose_and_long_k_head_grad():
     """The LM-head input gradient at the vocabulary K: E transposed to K-major (tw_transpose_bf16, exact,
     ragged edges) and the K = 51 904 product on the persistent kernel == the MN-major product on the 128x128
