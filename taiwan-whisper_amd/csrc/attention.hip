@@ -120,9 +120,13 @@ constexpr float NEG_BIG = -1e30f;
 // max tree (~26 VALU) and the O rescale (~20 VALU when some row max of the wave grew).
 constexpr float LZ_TH = 256.f;
 
-template <bool H, bool LZ>
+// ST: LDS ring depth.  2 = one tile in flight while the current one computes, then vmcnt(0) + barrier per tile;
+// 3 = two tiles in flight (prefetch distance 2: the DMA of tile kt+2 overlaps the compute of tiles kt and kt+1),
+// counted vmcnt + a raw s_barrier (a __syncthreads() would drain every DMA in flight).
+template <bool H, bool LZ, int ST = 2>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // [2 stages][K, V]
+  static_assert(ST == 2 || ST == 3, "ring depth");
+  __shared__ __attribute__((aligned(16))) char smem[ST * 2 * TB];   // [ST stages][K, V]
   const int lane = lane_id(), wave = wave_id_uniform();
   const int g = lane >> 4, li = lane & 15;
   int xblk, bh;
@@ -232,11 +236,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     }
   };
   stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (ST == 3) {
+    if (nkt > 1) {
+      stage(1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");      // tile 0 landed (4 DMA per tile per wave), tile 1 flies
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 
   for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+    const int cur = ST == 3 ? kt % 3 : (kt & 1);
     const char* Ks = smem + cur * 2 * TB;
     const char* Vs = Ks + TB;
     // all K and V fragments of this tile into registers BEFORE the next tile's LDS-DMA is
@@ -251,7 +265,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     for (int hj = 0; hj < 4; ++hj)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) vf[hj][ss] = rd_tr(Vs, hj * 16, ss, lane);
-    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    if constexpr (ST == 3) {
+      if (kt + 2 < nkt) stage((kt + 2) % 3, kt + 2);        // the slot tile kt-1 was read from
+    } else {
+      if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    }
     const int k0 = kt * KT;
     f32x4 s[4][2];
     scores(kf, s, k0);
@@ -303,8 +321,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
         o[hj][1] = mma16<H>(vf[hj][ss], p1, o[hj][1]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (ST == 3) {
+      // tile kt+1 must have landed for every wave; tile kt+2 (issued this iteration) may stay in flight
+      if (kt + 2 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // epilogue
@@ -853,8 +878,8 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
     // A/B benchmarking only: 0 = 16x16 kernel with the per-tile max (default), 1 = the 16x16 kernel with the
     // lazy max (enc self 1066 -> 1033 us, cross 363 -> 349 us, tools/bench_attn.py r03, but the dominant weight
     // of a row is then rounded too: the encoder output's share within 2 bf16 ulps of HF autocast fell below the
-    // 0.999 bound of tests/test_distill_gpu.py, so it stays opt-in), 4 / 8 = software-pipelined lazy-max 32x32
-    // kernel with that many waves per workgroup
+    // 0.999 bound of tests/test_distill_gpu.py, so it stays opt-in), 2 = the per-tile max with the round-3
+    // 2-stage K/V ring, 4 / 8 = software-pipelined lazy-max 32x32 kernel with that many waves per workgroup
     const char* e = getenv("TW_ATTN_FWD");
     return e ? atoi(e) : 0;
   }();
@@ -864,8 +889,12 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
     hipLaunchKernelGGL(attn_fwd32_kernel<8>, dim3((Tq + 255) / 256, B * H), dim3(512), 0, stream, p);
   } else if (variant == 1) {
     hipLaunchKernelGGL((attn_fwd_kernel<false, true>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  } else if (variant == 2) {
+    hipLaunchKernelGGL((attn_fwd_kernel<false, false, 2>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   } else {
-    hipLaunchKernelGGL((attn_fwd_kernel<false, false>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+    // 3-deep K/V ring (two tiles in flight): identical arithmetic to the 2-stage ring, enc self 1108 -> 1085 us,
+    // cross 384 -> 360 us (tools/bench_attn.py, same box, round 4)
+    hipLaunchKernelGGL((attn_fwd_kernel<false, false, 3>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   }
   TW_CHECK_LAUNCH();
   return TW_OK;
@@ -884,7 +913,7 @@ extern "C" int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
-  hipLaunchKernelGGL((attn_fwd_kernel<true, false>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((attn_fwd_kernel<true, false, 3>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -194,29 +194,6 @@ __device__ __forceinline__ void pp_epi_part(const GemmP& p, f32x4 (&acc)[8][4], 
 // prio 1 around each MFMA phase; 1 = the same with static prio 1 for the trailing wave row
 // (waves 4-7), no flips; 2 = diagnostic: every MFMA phase issued twice (wrong results; measures
 // the fixed per-phase cost); 4 = two 32-MFMA phases per K-tile (default: +4-8 % main loop)
-// s_waitcnt vmcnt(A) if `relax` (a wave-uniform scalar) is nonzero, else vmcnt(B).  The choice is a scalar branch
-// INSIDE the asm block, so the compiler sees straight-line code (a C++ branch here split the persistent kernel's
-// loop body and spilled it: 32 B of scratch per lane).
-template <int A, int B>
-__device__ __forceinline__ void wait_vm_sel(int relax) {
-  static_assert(A >= 0 && A < 64 && B >= 0 && B < 64, "vmcnt immediate");
-  asm volatile("s_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n\ts_waitcnt vmcnt(%1)\n\ts_branch 2f\n"
-               "1:\n\ts_waitcnt vmcnt(%2)\n2:" :: "s"(__builtin_amdgcn_readfirstlane(relax)), "n"(A), "n"(B)
-               : "memory", "scc");
-}
-
-// Store instructions (per lane) of the fast full-tile epilogue of a 256x256 tile (epilogue_fast, 8 fragment rows x
-// 4 fragment columns per wave): one 16-B store per fragment pair of a bf16 output, one per fragment of an fp32
-// output or of the GELU pre-activation side output.  The counted waits of the next tile's first K-tile pair leave
-// these stores in flight: they are younger than every LDS-DMA those waits are for, and s_waitcnt vmcnt counts loads,
-// stores and LDS-DMA together in issue order (MI355X_MICROARCH.md), so waiting for vmcnt(n + stores) completes the
-// same DMA as vmcnt(n) did before the stores -- without also waiting for the stores to be acknowledged.
-template <int KIND>
-constexpr int pp_epi_stores() {
-  return (KIND == EPI_STORE_BF16 || KIND == EPI_GELU || KIND == EPI_RES_BF16) ? 16
-       : (KIND == EPI_STORE_F32 || KIND == EPI_GELU_AUX || KIND == EPI_RES_F32) ? 32 : 0;
-}
-
 template <bool H, int PRIO, int KIND = -1>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   // + 2 x 1 KiB: the bias slice of the current tile (by tile parity), for the fast epilogue (one array:
@@ -231,8 +208,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const int total = my_tiles * nke;                       // K-tiles this workgroup consumes
 
   int si = 0;                                // current tile of this workgroup
-  constexpr int EPS = pp_epi_stores<KIND>();
-  int ep = 0;                                // 1: the previous pair ended with a fast epilogue's EPS stores
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -365,10 +340,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       // segment the A1 staged one segment-pair ago (6 DMA staged since), at a Y segment the
       // A0/B0/B1 staged one pair ago (2 since) — each published by the barriers before its
       // readers' segments.
-      if constexpr (PRIO != 7) {                                 // PRIO 7: diagnostic, no waits
-        if constexpr (EPS > 0) wait_vm_sel<6 + EPS, 6>(ep);
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      }
+      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // PRIO 7: diagnostic, no waits
       rdA(0, 0); rdB2(0); stg(cpa, cpb, cr, cc, ck, kt + 1, 1, 1);
       // a tile's first K-tile pair: wave 0 stages its 256 bias words (LDS-DMA, no registers).  The next-but-one
       // counted wait of wave 0 covers it and a barrier follows, long before the tile's epilogue reads it;
@@ -382,11 +354,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
         }
       }
       mma2(0);
-      if constexpr (PRIO != 7) {
-        if constexpr (EPS > 0) wait_vm_sel<2 + EPS, 2>(ep);
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
-      ep = 0;
+      if constexpr (PRIO != 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       if constexpr (PRIO == 4 || PRIO == 3) rdA(0, 1);      // PRIO 5: diagnostic, A-half 1 not read (LDS-read cost)
       stg(npa, npb, nr, nc, nkl, k2, 0, 0); stg(npa, npb, nr, nc, nkl, k2, 0, 2); stg(npa, npb, nr, nc, nkl, k2, 0, 3);
       mma2(1);
@@ -413,10 +381,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
     }
     if (last) {                                                 // tile finished
       pp_epi_part<H, KIND, 0, 8>(p, acc, si, wm, wn, lane, (const bf16*)(smem + 8 * PP_REGION + (si & 1) * 1024));
-      // the fast epilogue ran (the fp16 kernel runs full tiles only; bf16 ragged tiles take the generic one,
-      // whose store count varies: no relaxed wait after those; cr / cc = rows / columns left from the tile's
-      // corner) and stored (4096: diagnostic, no stores)
-      if constexpr (EPS > 0) ep = (!(p.flags & 4096) && (H || (cr >= 256 && cc >= 256))) ? 1 : 0;
       ++si;
     }
     cpa = npa; cpb = npb; cr = nr; cc = nc; ck = nkl;
@@ -853,6 +817,47 @@ int launch_sk_tail(GemmP p, int S, int m_dp, hipStream_t stream) {
   return 1;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Whole rounds persistent + a 128x128 tail: for grids whose last round of 256-tiles would leave most of the
+// persistent kernel's workgroups idle (the decoder's N = 1280 projections at M = 64 x 447: 560 256-tiles = 2.19
+// rounds, of which the third runs 48 tiles on 256 CUs), the m-tile rows of whole rounds run on the persistent
+// kernel and the remaining rows as 128x128 tiles on the 4-stage ring -- when they fit one round of it.  Both
+// kernels accumulate every output in the same K order (tests/test_kernels_gpu.py forced-tile identity), so the
+// result is bit-identical to either kernel alone.  Returns 0 (no plan) or 1, m_dp = m-tile rows of whole rounds.
+int dp_tail_plan(const GemmP& p, int batch, int& m_dp) {
+  if (batch != 1 || p.res_mod != 0) return 0;
+  const int G = pp_grid_cus();
+  const int tn = (p.N + 255) / 256, tm = (p.M + 255) / 256;
+  const int64_t T = (int64_t)tn * tm;
+  if (T < G || T >= 8 * G) return 0;
+  const int64_t rest = T % G;                            // 256-tiles of the last, partial round
+  if (rest == 0 || rest * 10 > (int64_t)G * 6) return 0;  // last round >= 60 % busy: keep it
+  m_dp = (int)((T / G) * G / tn);
+  const int rows = p.M - m_dp * 256;
+  const int64_t t128 = (int64_t)((rows + 127) / 128) * ((p.N + 127) / 128);
+  return (m_dp > 0 && rows > 0 && t128 <= G) ? 1 : 0;
+}
+
+template <bool H>
+int launch_dp_tail(const GemmP& p, int m_dp, hipStream_t stream) {
+  GemmP d = p;                                           // whole rounds: the persistent kernel
+  d.M = m_dp * 256;
+  launch_pp<H>(d, 1, stream);
+  TW_CHECK_LAUNCH();
+  GemmP q = p;                                           // the remaining rows: 128x128 tiles, 4-stage ring
+  const int64_t r0 = (int64_t)m_dp * 256;
+  const int csz = p.c_dtype == TW_BF16 ? 2 : 4;
+  q.A = p.A + r0 * p.lda;
+  q.M = p.M - (int)r0;
+  q.C = (char*)p.C + r0 * p.ldc * csz;
+  if (p.res) q.res = (const char*)p.res + r0 * p.ldr * (p.res_dtype == TW_BF16 ? 2 : 4);
+  if (p.aux) q.aux = p.aux + r0 * p.ldaux;
+  q.epi = pick_epilogue(q, 1);
+  launch<H, false, false, 128, 128, 2, 2, 4>(q, 1, stream);
+  TW_CHECK_LAUNCH();
+  return 1;
+}
+
 }  // namespace
 
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
@@ -912,6 +917,7 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   }();
   const bool dec_mid = !a_trans && !b_trans && batch == 1 && M < 65536 && N >= 2048 && N <= 4096 && K <= 2048;
   p.group_m = env_group > 0 ? env_group : (grouped ? 8 : (dec_mid && env_group_dec > 0 ? env_group_dec : 1));
+  if ((flags >> 24) & 15) p.group_m = (flags >> 24) & 15;     // forced tile order (A/B runs: tools/bench_group.py)
   p.epi = pick_epilogue(p, batch);
   // 256x256 tiles (8 waves) when the problem has enough tiles to fill the chip, else 128x128
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
@@ -1010,6 +1016,18 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     // (fp16: the persistent kernel runs full tiles only, so both parts must be whole 256-row blocks)
     const bool full = !H || ((N % 256) == 0 && ((M - m_dp * 256) % 256) == 0 && p.epi != EPI_GENERIC);
     if (S > 0 && full && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
+  }
+  // whole rounds persistent + a 128x128 tail (dp_tail_plan); TW_GEMM_DPTAIL=0 disables it (A/B runs)
+  static const int env_dpt = [] {
+    const char* e = getenv("TW_GEMM_DPTAIL");
+    return e ? atoi(e) : 1;
+  }();
+  if (!a_trans && !b_trans && env_dpt && !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
+    int m_dp = 0;
+    // (fp16: the persistent part must be whole 256x256 tiles with a fast epilogue)
+    if (dp_tail_plan(p, batch, m_dp) && (!H || ((N % 256) == 0 && p.epi != EPI_GENERIC)) &&
+        launch_dp_tail<H>(p, m_dp, stream))
+      return TW_OK;
   }
   // Grids of at most one 128x128 tile per CU (the 512-clip decode step's Linears: 40-160 tiles, one workgroup per
   // CU anyway) run on a 4-stage ring: three K-steps in flight instead of one hide the load latency that bounds a

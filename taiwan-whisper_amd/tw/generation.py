@@ -382,7 +382,11 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     cfg = model.config
     use_graph = True if use_graph is None else use_graph
     window = 2 * cfg.max_source_positions                     # 3000 feature frames = 30 s
-    if encoder_outputs is None and input_features is not None and input_features.shape[-1] > window:
+    # HF (generation_whisper.py:785-898) runs the seek loop for every input when timestamps are predicted, a
+    # <= 30 s one included: a window that ends on a timestamp pair before the end of the audio is followed by
+    # another window from that timestamp (tests/test_lv2_decode_gpu.py pins it at large-v2 dims)
+    seek_loop = bool(return_timestamps) and decoder_input_ids is None
+    if encoder_outputs is None and input_features is not None and (input_features.shape[-1] > window or seek_loop):
         return _longform(model, gc, input_features, attention_mask, language, task, max_length, max_new_tokens,
                          use_graph, window, kw.get("_trace"), fallback_batch=bool(kw.get("fallback_batch", True)), **fb)
     if kw.get("do_sample") or fb["temperature"] not in (0, 0.0) or fb["logprob_threshold"] is not None \

@@ -216,6 +216,44 @@ def test_gemm_forced_tiles_bit_identical(M, N, K):
             assert torch.equal(outs[name][kind], got), (name, kind)
 
 
+@pytest.mark.parametrize("M,N,K", [(28608, 1280, 1280), (14000, 2560, 640)])
+def test_gemm_dp_tail_bit_identical(M, N, K):
+    """Grids whose last round of 256-tiles would be mostly idle (the decoder's N = 1280 projections at B = 64:
+    560 256-tiles on 256 CUs) run whole rounds on the persistent kernel and the remaining rows as 128x128 tiles
+    (gemm.hip dp_tail_plan).  The default route must equal the 128x128 kernel alone bit for bit, for every
+    epilogue kind the step uses (bias + bf16 store, GELU + pre-activation, in-place bf16 / fp32 residual)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M + N)
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    bias, res = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    Ad, Wd, bd = bf(A).to(DEV), bf(W).to(DEV), bf(bias).to(DEV)
+    outs = {}
+    for name, f in (("dflt", 0), ("t128", ops.GEMM_TILE128)):
+        o = {}
+        Cb = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Ad, Wd, Cb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, flags=ops.GEMM_ROUND | f)
+        o["bf16"] = Cb
+        Cg, aux = torch.empty_like(Cb), torch.empty_like(Cb)
+        ops.gemm(Ad, Wd, Cg, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, aux=aux, ldaux=N,
+                 flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT | f)
+        o["gelu"], o["aux"] = Cg, aux
+        rb = bf(res).to(DEV)
+        ops.gemm(Ad, Wd, rb, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rb, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_bf16"] = rb
+        rf = res.clone().to(DEV)
+        ops.gemm(Ad, Wd, rf, M, N, K, lda=K, ldb=K, ldc=N, bias=bd, res=rf, ldr=N, flags=ops.GEMM_ROUND | f)
+        o["res_f32"] = rf
+        torch.cuda.synchronize()
+        outs[name] = o
+    for kind in outs["t128"]:
+        assert not torch.isnan(outs["dflt"][kind].float()).any(), kind
+        assert torch.equal(outs["dflt"][kind], outs["t128"][kind]), kind
+    rows = torch.tensor([0, M // 2, M - 300, M - 1])
+    ref = bf((bf(A[rows]).double() @ bf(W).double().T + bf(bias).double()).float()).float()
+    got = outs["dflt"]["bf16"][rows.to(DEV)].float().cpu()
+    assert (got - ref).abs().max() <= 2 ** -7 * ref.abs().max()
+
+
 @pytest.mark.parametrize("M,N,K", [(8200, 2056, 320), (8200, 2056, 128), (4104, 4096, 1344), (520, 264, 64),
                                    (2312, 1288, 5128), (8200, 4104, 1344), (16400, 2056, 256)])
 def test_gemm_pp_persistent_ragged(M, N, K):
