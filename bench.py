@@ -489,7 +489,9 @@ def main():
                                "gemm_pp_kernel (persistent 256x256 ping-pong, + split-K tail) + "
                                "gemm_kernel<false,false,128,...> for grids under ~1000 256-tiles",
                         launches_per_step=ks["launches"] // args.steps, avg_launch_ms=round(ks["avg_ms"], 4),
-                        algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4))
+                        algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4),
+                        algo_bytes_per_launch=round(ks["avg_bytes"]),
+                        traffic_over_algo=(round(pmc / ks["avg_bytes"], 3) if pmc and ks["avg_bytes"] else None))
         out = {
             "metric": "distillation utterances/sec (30 s clips)",
             "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,

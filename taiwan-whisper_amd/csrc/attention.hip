@@ -108,6 +108,8 @@ __device__ __forceinline__ void remap_bh(int& xblk, int& bh) {
 }
 constexpr float NEG_BIG = -1e30f;
 
+__device__ __forceinline__ float fmx(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
 // ------------------------------------------------------------------------------------
 // H = false: bf16 Q/K/V/O (autocast); H = true: fp16 (the fp16 decode path: P rounded to fp16 for PV,
 // as SDPA's fp16 flash kernel rounds it)
@@ -169,13 +171,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
   auto scores = [&](const bf16x8 (&kf)[4][2], f32x4 (&s)[4][2], int k0) {
 #pragma unroll
     for (int kj = 0; kj < 4; ++kj) {
-      s[kj][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      s[kj][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        s[kj][0] = mma16<H>(kf[kj][kk], qf[0][kk], s[kj][0]);
-        s[kj][1] = mma16<H>(kf[kj][kk], qf[1][kk], s[kj][1]);
-      }
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      s[kj][0] = mma16<H>(kf[kj][1], qf[0][1], mma16<H>(kf[kj][0], qf[0][0], z));
+      s[kj][1] = mma16<H>(kf[kj][1], qf[1][1], mma16<H>(kf[kj][0], qf[1][0], z));
     }
     const bool need_mask = (k0 + KT > p.Tk) || (p.causal && k0 + KT - 1 > qw + off);
     if (need_mask) {
@@ -201,16 +199,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     for (int qi = 0; qi < 2; ++qi) {
       // row max: a tree over the lane's 16 scores, then across the 4 lanes of the query column
       // (l, l^16, l^32, l^48) with v_permlane16/32_swap (VALU) instead of two ds_bpermute trips
-      float t4[4];
+      // (a chain of 3-input maxes: 8 v_maximum3_f32 for the 16 scores.  IEEE maximum, not fmaxf: fmaxf in the
+      // kernels' IEEE mode first quiets each MFMA result with a v_max_f32 x, x; maximum needs none and propagates
+      // a NaN score, which the weights would carry to O and l anyway)
+      float tmax = fmx(fmx(s[0][qi][0], s[0][qi][1]), s[0][qi][2]);
 #pragma unroll
-      for (int kj = 0; kj < 4; ++kj)
-        t4[kj] = fmaxf(fmaxf(s[kj][qi][0], s[kj][qi][1]), fmaxf(s[kj][qi][2], s[kj][qi][3]));
-      float tmax = fmaxf(fmaxf(t4[0], t4[1]), fmaxf(t4[2], t4[3]));
+      for (int e = 3; e < 15; e += 2)
+        tmax = fmx(fmx(tmax, s[e >> 2][qi][e & 3]), s[(e + 1) >> 2][qi][(e + 1) & 3]);
+      tmax = fmx(tmax, s[3][qi][3]);
       {
         const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-        tmax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        tmax = fmx(__uint_as_float(a[0]), __uint_as_float(a[1]));
         const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-        tmax = fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+        tmax = fmx(__uint_as_float(c[0]), __uint_as_float(c[1]));
       }
       const float mn = fmaxf(m[qi], tmax * p.scale_log2);
       if (__any(mn > m[qi])) {
@@ -352,251 +353,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
   }
 }
 
-
-// ------------------------------------------------------------------------------------
-// Forward, 32x32x16 form.  S^T = K·Q^T with v_mfma_f32_32x32x16_bf16 (A = K rows, B = Q rows):
-// lane l holds query l&31 and, per 32-key block, keys 8j + 4h + r (h = l>>5, j,r = 0..3), so a
-// query's 64 scores of a tile sit in 2 lanes (l, l^32): the row max is 31 lane-local max
-// ops + one v_permlane32_swap, the row sum stays lane-local until the end.  O^T += V^T·P^T
-// consumes P straight from those registers: k-step u (16 keys) takes keys
-// 16u + 8(i>>2) + 4h + (i&3) (i = 0..7) = scores s[u>>1][8(u&1) + i], and the V^T operand reads
-// the same keys with two ds_read_b64_tr_b16 (rows 16u+4h.., 16u+8+4h..).
-// LDS images ([64 keys][64] bf16, 128-B rows, 16-B chunk c of row r at c ^ f(r)):
-//   K: f(r) = (r >> 1) & 7        -> the 32-row ds_read_b128 reads are conflict-free
-//   V: f(r) = ((r >> 1) & 1) << 2 -> the 4-row x 64-B ds_read_b64_tr_b16 halves are conflict-free
-// K/V arrive by LDS-DMA into a 3-deep ring (prefetch distance 2, counted vmcnt, raw barrier).
-// NW waves x 32 queries per workgroup share every K/V tile.
-// ------------------------------------------------------------------------------------
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-__device__ __forceinline__ int fk32(int r) { return (r >> 1) & 7; }
-__device__ __forceinline__ int fv32(int r) { return ((r >> 1) & 1) << 2; }
-
-// [64][64] tile rows row0.. -> LDS, swizzle F; rows >= rows_valid read 0.  8 pieces of 1 KiB.
-template <int NW, bool ISV>
-__device__ __forceinline__ void stage32(const bf16* base, int64_t ld, int rows_valid, char* lds, int wave, int lane) {
-  const auto rs = make_rsrc(base);
-#pragma unroll
-  for (int i = 0; i < 8 / NW; ++i) {
-    const int pce = wave + NW * i;
-    const int r = pce * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (ISV ? fv32(r) : fk32(r));
-    const uint32_t off = r < rows_valid ? (uint32_t)(((int64_t)r * ld + c * 8) * 2) : TW_OOB;
-    buf_load_lds16(rs, lds + pce * 1024, off);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else static_assert(N < 0, "add the vmcnt immediate");
-}
-
-// Software-pipelined: the S MFMAs of tile kt+1 are issued before the softmax of tile kt, so the
-// matrix pipe runs under the softmax VALU work of the same wave.  Lazy max: scores are
-// exponentiated against the running max m; only when some lane's partial sum leaves
-// (0, 2^8] (a new max more than 8 above m, or the first tile against m = -1e30) does the wave
-// take the exact path (tile max, rescale O and l, re-exponentiate).  P <= 2^8 before
-// normalisation changes nothing but where bf16 rounds it (same relative precision).
-// Ring: tile kt's V and tile kt+1's K are read in iteration kt, tile kt+2 is staged; vmcnt(0)
-// + barrier at the end of each iteration, so no LDS-DMA is in flight while fragments are read.
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnP p) {
-  constexpr int ST = 3;                         // LDS ring depth
-  __shared__ __attribute__((aligned(16))) char smem[ST * 2 * TB];
-  const int lane = lane_id(), wave = wave_id_uniform();
-  const int h = lane >> 5, q32 = lane & 31, G = lane >> 4, t16 = lane & 15;
-  int xblk, bh;
-  remap_bh(xblk, bh);
-  const int b = bh / p.H, hd = bh % p.H;
-  const int qblk = xblk * NW * 32;
-  const int qw = qblk + wave * 32;
-  const bf16* Qb = p.Q + (int64_t)b * p.Tq * p.ldq + hd * 64;
-  const bf16* Kb = p.K + (int64_t)b * p.Tk * p.ldk + hd * 64;
-  const bf16* Vb = p.V + (int64_t)b * p.Tk * p.ldv + hd * 64;
-  const int off = p.Tk - p.Tq;
-  const float c2 = p.scale_log2;
-
-  int nkt = (p.Tk + KT - 1) / KT;
-  if (p.causal) {
-    const int qmax = min(p.Tq - 1, qblk + NW * 32 - 1);
-    nkt = min(nkt, (qmax + off + 1 + KT - 1) / KT);
-  }
-  auto stage = [&](int buf, int kt) {
-    char* Ks = smem + buf * 2 * TB;
-    const int k0 = kt * KT;
-    stage32<NW, false>(Kb + (int64_t)k0 * p.ldk, p.ldk, p.Tk - k0, Ks, wave, lane);
-    stage32<NW, true>(Vb + (int64_t)k0 * p.ldv, p.ldv, p.Tk - k0, Ks + TB, wave, lane);
-  };
-  auto read_k = [&](const char* Ks, bf16x8 (&kf)[2][4]) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int r = kb * 32 + q32, c = kk * 2 + h;
-        kf[kb][kk] = *(const bf16x8*)(Ks + r * 128 + ((c ^ fk32(r)) << 4));
-      }
-  };
-  auto read_v = [&](const char* Vs, bf16x8 (&vf)[2][4]) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int col = db * 32 + (G & 1) * 16 + 4 * (t16 & 3);
-        const int r0 = u * 16 + 4 * h + (t16 >> 2), r1 = r0 + 8;
-        const int ch = col >> 3, inoff = (col & 7) * 2;
-        const char* a0 = Vs + r0 * 128 + ((ch ^ fv32(r0)) << 4) + inoff;
-        const char* a1 = Vs + r1 * 128 + ((ch ^ fv32(r1)) << 4) + inoff;
-        s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
-        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a1);
-        vf[db][u] = __builtin_bit_cast(bf16x8, s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
-      }
-  };
-
-  stage(0, 0);
-  if (nkt > 1) stage(1, 1);
-  // Q^T operand: lane gives Q[qw + q32][16kk + 8h .. +7]
-  bf16x8 qf[4];
-  {
-    const int q = qw + q32;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      qf[kk] = q < p.Tq ? *(const bf16x8*)(Qb + (int64_t)q * p.ldq + kk * 16 + 8 * h) : bf16x8{};
-  }
-  auto s_mma = [&](const bf16x8 (&kf)[2][4], f32x16 (&sc)[2]) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) sc[kb][j] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], sc[kb], 0, 0, 0);
-    }
-  };
-  f32x16 o[2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) o[db][j] = 0.f;
-  float m = NEG_BIG, l4[4] = {0.f, 0.f, 0.f, 0.f};
-
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  f32x16 sA[2], sB[2];
-  {
-    bf16x8 kf[2][4];
-    read_k(smem, kf);
-    s_mma(kf, sA);
-  }
-
-  // softmax of one tile (scores sc, keys k0..) + PV with that tile's V fragments
-  auto softmax_pv = [&](f32x16 (&sc)[2], const int k0, const bf16x8 (&vf)[2][4]) {
-    if ((k0 + KT > p.Tk) || (p.causal && k0 + KT - 1 > qw + off)) {
-      const int q = qw + q32;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int key = k0 + kb * 32 + 8 * (j >> 2) + 4 * h + (j & 3);
-          if (!(key < p.Tk && (!p.causal || key <= q + off))) sc[kb][j] = -INFINITY;
-        }
-    }
-    f32x16 e[2];
-    float ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        e[kb][j] = __builtin_amdgcn_exp2f(fmaf(sc[kb][j], c2, -m));
-        ps[j & 3] += e[kb][j];
-      }
-    float pt = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-    if (__any(!(pt <= 256.f))) {                // rare: exact max, rescale, re-exponentiate
-      float t8[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int kb = i >> 2, j = 4 * (i & 3);
-        t8[i] = fmaxf(fmaxf(sc[kb][j], sc[kb][j + 1]), fmaxf(sc[kb][j + 2], sc[kb][j + 3]));
-      }
-      float tmax =
-          fmaxf(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])), fmaxf(fmaxf(t8[4], t8[5]), fmaxf(t8[6], t8[7])));
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-      tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      const float mn = fmaxf(m, tmax * c2);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) l4[i] *= alpha;
-#pragma unroll
-      for (int db = 0; db < 2; ++db) o[db] *= alpha;
-      m = mn;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ps[i] = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          e[kb][j] = __builtin_amdgcn_exp2f(fmaf(sc[kb][j], c2, -m));
-          ps[j & 3] += e[kb][j];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) l4[i] += ps[i];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int kb = u >> 1, j0 = 8 * (u & 1);
-      const bf16x8 pf = bf16x8{f2bf(e[kb][j0 + 0]), f2bf(e[kb][j0 + 1]), f2bf(e[kb][j0 + 2]), f2bf(e[kb][j0 + 3]),
-                               f2bf(e[kb][j0 + 4]), f2bf(e[kb][j0 + 5]), f2bf(e[kb][j0 + 6]), f2bf(e[kb][j0 + 7])};
-#pragma unroll
-      for (int db = 0; db < 2; ++db) o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db][u], pf, o[db], 0, 0, 0);
-    }
-  };
-
-  // iteration kt (ring slot SLOT = kt % 3): V_kt and K_{kt+1} read, tile kt+2 staged, S_{kt+1}
-  // issued, then softmax + PV of tile kt.  Unrolled by 6 (ring slot x S register set).
-  auto iter = [&](const int kt, auto slot_c, f32x16 (&scur)[2], f32x16 (&snxt)[2]) {
-    constexpr int SLOT = decltype(slot_c)::value;
-    bf16x8 vf[2][4];
-    read_v(smem + SLOT * 2 * TB + TB, vf);
-    const bool more = kt + 1 < nkt;
-    bf16x8 kf[2][4];
-    if (more) read_k(smem + ((SLOT + 1) % ST) * 2 * TB, kf);
-    if (kt + 2 < nkt) stage((SLOT + 2) % ST, kt + 2);
-    if (more) s_mma(kf, snxt);
-    softmax_pv(scur, kt * KT, vf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int kt = 0; kt < nkt; kt += 6) {
-    iter(kt, std::integral_constant<int, 0>{}, sA, sB);
-    if (kt + 1 < nkt) iter(kt + 1, std::integral_constant<int, 1>{}, sB, sA);
-    if (kt + 2 < nkt) iter(kt + 2, std::integral_constant<int, 2>{}, sA, sB);
-    if (kt + 3 < nkt) iter(kt + 3, std::integral_constant<int, 0>{}, sB, sA);
-    if (kt + 4 < nkt) iter(kt + 4, std::integral_constant<int, 1>{}, sA, sB);
-    if (kt + 5 < nkt) iter(kt + 5, std::integral_constant<int, 2>{}, sB, sA);
-  }
-
-  // epilogue: row sum across the lane pair, O^T -> O rows (lane holds d = 32db + 8j + 4h + r)
-  float l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-    l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-  }
-  const int q = qw + q32;
-  if (q < p.Tq) {
-    const float inv = 1.f / l;
-    bf16* Ob = p.O + ((int64_t)b * p.Tq + q) * p.ldo + hd * 64;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int d = db * 32 + 8 * j + 4 * h;
-        *(bf16x4*)(Ob + d) = bf16x4{f2bf(o[db][4 * j] * inv), f2bf(o[db][4 * j + 1] * inv),
-                                    f2bf(o[db][4 * j + 2] * inv), f2bf(o[db][4 * j + 3] * inv)};
-      }
-    if (h == 0 && p.lse) p.lse[(int64_t)bh * p.Tq + q] = (m + log2f(l)) / LOG2E;
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // D[b,h,q] = sum_e dO[q][e] * O[q][e]     (one wave per (row, head))
@@ -879,15 +635,11 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
     // lazy max (enc self 1066 -> 1033 us, cross 363 -> 349 us, tools/bench_attn.py r03, but the dominant weight
     // of a row is then rounded too: the encoder output's share within 2 bf16 ulps of HF autocast fell below the
     // 0.999 bound of tests/test_distill_gpu.py, so it stays opt-in), 2 = the per-tile max with the round-3
-    // 2-stage K/V ring, 4 / 8 = software-pipelined lazy-max 32x32 kernel with that many waves per workgroup
+    // 2-stage K/V ring.  (The round-2/3 32x32x16 software-pipelined kernel, no faster, was deleted in round 4.)
     const char* e = getenv("TW_ATTN_FWD");
     return e ? atoi(e) : 0;
   }();
-  if (variant == 4) {
-    hipLaunchKernelGGL(attn_fwd32_kernel<4>, dim3((Tq + 127) / 128, B * H), dim3(256), 0, stream, p);
-  } else if (variant == 8) {
-    hipLaunchKernelGGL(attn_fwd32_kernel<8>, dim3((Tq + 255) / 256, B * H), dim3(512), 0, stream, p);
-  } else if (variant == 1) {
+  if (variant == 1) {
     hipLaunchKernelGGL((attn_fwd_kernel<false, true>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   } else if (variant == 2) {
     hipLaunchKernelGGL((attn_fwd_kernel<false, false, 2>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);

@@ -929,6 +929,18 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   // very long K (the LM-head input gradient, K = 51 904): the persistent kernel wins from one round up
   // (3356 vs 4006 us on 560 tiles, tools/bench_head_bwd.py), its per-tile fixed cost being amortised
   if (!a_trans && !b_trans && K >= 8192 && t256 >= pp_grid_cus()) tile = 256;
+  // K-major forward grids of 1-4 rounds whose rounds are well filled (c2's B = 32 shapes: the teacher encoder's
+  // N = 1280 Linears at M = 48 000, 940 256-tiles = 3.67 rounds, 92 % of the workgroup-rounds busy; the student
+  // decoder's fused QKV and fc1): the persistent kernel.  Grids with a mostly idle last round take the whole-round
+  // + 128x128 tail split below (dp_tail_plan).  TW_PP_MINFILL (percent, A/B runs): the fill threshold.
+  static const int env_minfill = [] {
+    const char* e = getenv("TW_PP_MINFILL");
+    return e ? atoi(e) : 85;
+  }();
+  if (!a_trans && !b_trans && tile == 128 && K >= 256 && env_minfill <= 100) {
+    const int64_t G = pp_grid_cus();
+    if (t256 >= G && t256 * 100 >= ((t256 + G - 1) / G) * G * env_minfill) tile = 256;
+  }
   if (tile == 256 && !a_trans && !b_trans) tile = 2562;
   if (flags & 256) tile = 128;        // forced tile (benchmarking / A-B comparisons)
   if (flags & 512) tile = 256;

@@ -329,14 +329,16 @@ __device__ __forceinline__ float hi_e(uint32_t u) {
   else return __builtin_bit_cast(float, u & 0xffff0000u);
 }
 
-// fragments X (ni) and Y (ni+1), 4 floats each -> this lane's 16 B of the pair (swapped layout)
-template <bool H>
-__device__ __forceinline__ u32x4 pair_to_u4(const float (&x)[4], const float (&y)[4]) {
-  const uint32_t x0 = pack2<H>(x[0], x[1]), x1 = pack2<H>(x[2], x[3]);
-  const uint32_t y0 = pack2<H>(y[0], y[1]), y1 = pack2<H>(y[2], y[3]);
+// packed fragments X (ni) and Y (ni+1), 2 words each -> this lane's 16 B of the pair (swapped layout)
+__device__ __forceinline__ u32x4 swap_u4(uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1) {
   const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
   return u32x4{s0[0], s1[0], s0[1], s1[1]};
+}
+// fragments X (ni) and Y (ni+1), 4 floats each -> this lane's 16 B of the pair (swapped layout)
+template <bool H>
+__device__ __forceinline__ u32x4 pair_to_u4(const float (&x)[4], const float (&y)[4]) {
+  return swap_u4(pack2<H>(x[0], x[1]), pack2<H>(x[2], x[3]), pack2<H>(y[0], y[1]), pack2<H>(y[2], y[3]));
 }
 // inverse: this lane's 16 B of the pair (swapped layout) -> fragments X, Y as floats
 template <bool H>
@@ -439,11 +441,24 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
           *(f32x4*)(crow + (2 * np + h) * 16 + 4 * g) = o;
         }
       } else if constexpr (KIND == EPI_GELU || KIND == EPI_GELU_AUX) {
+        // autocast: the Linear output is bf16.  GELU only: one v_cvt_pk per two values, unpacked (rnd<H> of each
+        // value, bit for bit; 2102 vs 2250 instructions per tile and wave, 56 vs 141 s_nop).  With the aux output
+        // the per-value rounding stays: swapping the freshly packed words for the aux store serialised the GELU
+        // chains (2783 vs 2563 instructions, 623 vs 275 s_nop).
+        if constexpr (KIND == EPI_GELU) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t w0 = pack2<H>(v[h][0], v[h][1]), w1 = pack2<H>(v[h][2], v[h][3]);
+            v[h][0] = lo_e<H>(w0);
+            v[h][1] = hi_e<H>(w0);
+            v[h][2] = lo_e<H>(w1);
+            v[h][3] = hi_e<H>(w1);
+          }
+        } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[h][r] = rnd<H>(v[h][r]);     // autocast: Linear output is bf16
-        if constexpr (KIND == EPI_GELU_AUX) {
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[h][r] = rnd<H>(v[h][r]);
           bf16* arow = p.aux + bz * p.sAux + m * p.ldaux + cw;
           *(u32x4*)(arow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
         }

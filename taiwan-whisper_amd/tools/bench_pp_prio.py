@@ -1,6 +1,7 @@
 """A/B of the persistent ping-pong GEMM's issue-priority schemes (gemm_pp_kernel<PRIO>, flags bits 15-16)
 and its epilogue cost (p4e: no epilogue, p4z: the epilogue computed and stored into tile 0 -- L2-resident
-stores, no HBM write traffic; diagnostic flags),
+stores, no HBM write traffic; p4s: the epilogue computed, nothing stored -- needs tools/patches/pp_epilogue_nostore_diag.patch applied, and
+that build perturbs the epilogue code (per-store branches); diagnostic flags),
 interleaved in one process on random data, forward shapes of the distillation step."""
 import os
 import sys
@@ -14,7 +15,7 @@ SHAPES = [("enc qkv", 96000, 3840, 1280, 0), ("enc out", 96000, 1280, 1280, 0), 
           ("enc fc2", 96000, 1280, 5120, 0), ("xattn kv", 96000, 2560, 1280, 0), ("dec fc1", 28608, 5120, 1280, 1),
           ("lm head", 28608, 51904, 1280, 0)]
 VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "p4,p0,p4e").split(",")
-FLAG = {"p4": 0, "p4e": 4096, "p4z": 1 << 20, "p0": 1 << 15, "p0e": (1 << 15) | 4096,
+FLAG = {"p4": 0, "p4e": 4096, "p4z": 1 << 20, "p4s": 1 << 21, "p0": 1 << 15, "p0e": (1 << 15) | 4096,
         "p2x": 2 << 15, "p2xe": (2 << 15) | 4096, "p1": 3 << 15, "p5e": (5 << 15) | 4096, "p6e": (6 << 15) | 4096, "p7e": (7 << 15) | 4096}
 
 

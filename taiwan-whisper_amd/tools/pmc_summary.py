@@ -6,12 +6,12 @@ kernel stages operands with 16-B buffer_load ... lds); WRITE_SIZE is exact for 1
 8-B stores are uncalibrated).  Infinity-Cache hits appear to be counted, so this is an upper bound
 of DRAM bytes.
 
-A third, optional pass records TCC_EA0_RDREQ_sum and TCC_EA0_RDREQ_DRAM_sum (read requests "destined for
-DRAM").  Measured r02: the two are equal for every kernel family (share 1.000), i.e. the counter is taken
-before the Infinity Cache (MALL), so it does not split MALL hits from HBM reads; fetch stays an upper
-bound of DRAM bytes.
+No counter on gfx950 splits Infinity-Cache (MALL) hits from HBM reads: TCC_EA0_RDREQ_DRAM_sum equals
+TCC_EA0_RDREQ_sum for every kernel family (measured r02, share 1.000 - the request is counted before the
+MALL), so the former dram_* fields were copies of the fetch and are no longer reported.  The figures are
+L2-miss traffic (the L2 <-> fabric bytes), an upper bound of DRAM bytes.
 
-usage: python pmc_summary.py <fetch_dir> <write_dir> <out.json> [<dram_dir>]
+usage: python pmc_summary.py <fetch_dir> <write_dir> <out.json>
 """
 import csv
 import json
@@ -23,7 +23,6 @@ FAMILIES = {
     "gemm_nn": r"gemm_kernel<false, false|gemm_pp_kernel",
     "gemm_nt": r"gemm_kernel<false, true",
     "gemm_tt": r"gemm_kernel<true, true",
-    "vendor_gemm": r"Cijk_",                     # hipBLASLt kernels (csrc/gemm_vendor.hip)
     "attn_fwd": r"attn_fwd_kernel",
     "klce": r"klce_kernel",
     "ln_fwd": r"ln_fwd_kernel",
@@ -44,10 +43,7 @@ def load(d, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
-    ddir = sys.argv[4] if len(sys.argv) > 4 else None
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
-    rq = load(ddir, "TCC_EA0_RDREQ_sum") if ddir else {}
-    rqd = load(ddir, "TCC_EA0_RDREQ_DRAM_sum") if ddir else {}
     res = {}
     for fam in FAMILIES:
         if not fetch.get(fam) or not write.get(fam):
@@ -56,17 +52,11 @@ def main():
         w = sum(write[fam]) / len(write[fam]) * 1024
         res[fam] = dict(launches=len(fetch[fam]), fetch_bytes_per_launch=f, write_bytes_per_launch=w,
                         hbm_bytes_per_launch=f + w)
-        extra = ""
-        if rq.get(fam) and rqd.get(fam) and sum(rq[fam]) > 0:
-            share = sum(rqd[fam]) / sum(rq[fam])
-            res[fam]["dram_read_share"] = share
-            res[fam]["dram_fetch_bytes_per_launch"] = f * share
-            res[fam]["dram_bytes_per_launch"] = f * share + w
-            extra = f"  DRAM share of reads {share:.3f} -> {f * share / 1e6:9.1f} MB from DRAM"
-        print(f"{fam:9s} launches={len(fetch[fam]):5d} fetch {f/1e6:9.1f} MB  write {w/1e6:9.1f} MB per launch{extra}")
+        print(f"{fam:9s} launches={len(fetch[fam]):5d} fetch {f/1e6:9.1f} MB  write {w/1e6:9.1f} MB per launch")
     res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over `bench.py --steps 2 --warmup 1`; "
-                    "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; the fetch counts Infinity-Cache hits too "
-                    "(MI355X_MICROARCH.md): dram_* split it by TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ from a third pass")
+                    "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes.  L2-miss (L2 <-> fabric) bytes: "
+                    "Infinity-Cache hits are counted too and no gfx950 counter separates them, so hbm_bytes_per_launch "
+                    "is an upper bound of DRAM bytes")
     json.dump(res, open(out, "w"), indent=1)
 
 

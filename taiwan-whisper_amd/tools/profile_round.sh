@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round-end evidence on a 1-GPU box (run from the repo root through gpurun):
-#   1. FETCH_SIZE, WRITE_SIZE and TCC_EA0_RDREQ(_DRAM) passes over a short bench run (separate --pmc runs,
-#      kernel trace off)
+#   1. FETCH_SIZE and WRITE_SIZE passes over a short bench run (separate --pmc runs, kernel trace off)
 #      -> profiles/pmc_latest.json via pmc_summary.py (gfx950 corrections there)
 #   2. kernel-trace + stats of the same bench command -> gpurun_out/prof/run_kernel_stats.csv
 #   3. the default bench line (with the CPU baseline) -> gpurun_out/bench.log
@@ -18,9 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fet
 echo "fetch pass done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $BENCH > $OUT/pmc_write.log 2>&1
 echo "write pass done"
-timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum --output-format csv -d $OUT/pmc_dram -o run -- python3 $BENCH > $OUT/pmc_dram.log 2>&1
-echo "dram pass done"
-python3 $R/taiwan-whisper_amd/tools/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_$TAG.json $OUT/pmc_dram
+python3 $R/taiwan-whisper_amd/tools/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1
 echo "trace pass done"
 cd $R

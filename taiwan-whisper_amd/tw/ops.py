@@ -86,10 +86,13 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
         _need(aux, (batch - 1) * sAux + (M - 1) * ldaux + N, "gemm aux")
     fam = "gemm_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
     flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
+    eh, ec = A.element_size(), C.element_size()
+    nbytes = batch * (eh * (M * K + N * K) + ec * M * N + (res.element_size() * M * N if res is not None else 0)
+                      + (eh * M * N if aux is not None else 0))
     KernelTimer.wrap(fam, flops, lambda: call(
         "tw_gemm_f16" if h == torch.float16 else "tw_gemm_bf16", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, _dt(C),
         M, N, K, batch, sA, sB, sC, float(alpha), _ptr(bias), _ptr(res), ldr, sR,
-        _dt(res) if res is not None else F32, res_mod, _ptr(aux), ldaux, sAux, flags, _stream()))
+        _dt(res) if res is not None else F32, res_mod, _ptr(aux), ldaux, sAux, flags, _stream()), nbytes)
     return C
 
 
@@ -546,10 +549,13 @@ def gemm_f32(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, a
         _need(aux, (nb - 1) * sAux + (M - 1) * ldaux + N, "gemm_f32 aux")
     fam = "gemm32_" + ("t" if a_trans else "n") + ("t" if b_trans else "n")
     flops = 2.0 * M * (N if algo_N is None else algo_N) * K * batch
+    eh, ec = A.element_size(), C.element_size()
+    nbytes = batch * (eh * (M * K + N * K) + ec * M * N + (res.element_size() * M * N if res is not None else 0)
+                      + (eh * M * N if aux is not None else 0))
     KernelTimer.wrap(fam, flops, lambda: call(
         "tw_gemm_f32", A.data_ptr(), lda, int(a_trans), B.data_ptr(), ldb, int(b_trans), C.data_ptr(), ldc, M, N, K,
         batch, sA, sB, sC, batch_inner, sA_in, sB_in, sC_in, float(alpha), _ptr(bias), _ptr(res), ldr, sR, res_mod,
-        _ptr(aux), ldaux, sAux, flags, _stream()))
+        _ptr(aux), ldaux, sAux, flags, _stream()), nbytes)
     return C
 
 

@@ -22,6 +22,9 @@ DEV = "cuda"
 def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
+    # the operators register on import of tw.torch_ops; a test selection that runs only this module's opcheck
+    # cases must not depend on another test having imported it first
+    import tw.torch_ops  # noqa: F401
 
 
 def _v3(t, B, T, off, C):
