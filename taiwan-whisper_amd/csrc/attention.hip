@@ -113,21 +113,12 @@ __device__ __forceinline__ float fmx(float a, float b) { return __builtin_elemen
 // ------------------------------------------------------------------------------------
 // H = false: bf16 Q/K/V/O (autocast); H = true: fp16 (the fp16 decode path: P rounded to fp16 for PV,
 // as SDPA's fp16 flash kernel rounds it)
-// LZ = true: lazy max.  A tile is exponentiated against the running max m without computing its own max;
-// a lane whose partial sum of the 16 weights of one query leaves [0, LZ_TH] (a score more than
-// log2(LZ_TH / 16) = 4 above m in the log2 domain, the first tile against m = -1e30, or a NaN) sends the
-// wave down the exact path: S recomputed from the K tile still in LDS (the weights overwrote it), the tile
-// max, the O / l rescale, the weights again.  Weights are then <= LZ_TH before normalisation: bf16 / fp16
-// round them with the same relative precision, and m + log2(l) is the same LSE.  Saves the per-tile
-// max tree (~26 VALU) and the O rescale (~20 VALU when some row max of the wave grew).
-constexpr float LZ_TH = 256.f;
-
-// ST: LDS ring depth.  2 = one tile in flight while the current one computes, then vmcnt(0) + barrier per tile;
-// 3 = two tiles in flight (prefetch distance 2: the DMA of tile kt+2 overlaps the compute of tiles kt and kt+1),
-// counted vmcnt + a raw s_barrier (a __syncthreads() would drain every DMA in flight).
-template <bool H, bool LZ, int ST = 2>
+// K/V arrive in a 3-deep LDS ring: two tiles in flight (prefetch distance 2: the DMA of tile kt+2 overlaps the
+// compute of tiles kt and kt+1), counted vmcnt + a raw s_barrier (a __syncthreads() would drain every DMA in
+// flight).  (Round 3's opt-in lazy max and the 2-stage ring were deleted in round 4: DESIGN.md, Attention.)
+template <bool H>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
-  static_assert(ST == 2 || ST == 3, "ring depth");
+  constexpr int ST = 3;
   __shared__ __attribute__((aligned(16))) char smem[ST * 2 * TB];   // [ST stages][K, V]
   const int lane = lane_id(), wave = wave_id_uniform();
   const int g = lane >> 4, li = lane & 15;
@@ -237,21 +228,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     }
   };
   stage(0, 0);
-  if constexpr (ST == 3) {
-    if (nkt > 1) {
-      stage(1, 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");      // tile 0 landed (4 DMA per tile per wave), tile 1 flies
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
+  if (nkt > 1) {
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");      // tile 0 landed (4 DMA per tile per wave), tile 1 flies
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  __builtin_amdgcn_s_barrier();
 
   for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = ST == 3 ? kt % 3 : (kt & 1);
+    const int cur = kt % 3;
     const char* Ks = smem + cur * 2 * TB;
     const char* Vs = Ks + TB;
     // all K and V fragments of this tile into registers BEFORE the next tile's LDS-DMA is
@@ -266,49 +252,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
     for (int hj = 0; hj < 4; ++hj)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) vf[hj][ss] = rd_tr(Vs, hj * 16, ss, lane);
-    if constexpr (ST == 3) {
-      if (kt + 2 < nkt) stage((kt + 2) % 3, kt + 2);        // the slot tile kt-1 was read from
-    } else {
-      if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
-    }
+    if (kt + 2 < nkt) stage((kt + 2) % 3, kt + 2);          // the slot tile kt-1 was read from
     const int k0 = kt * KT;
     f32x4 s[4][2];
     scores(kf, s, k0);
     float ls[2];
-    if constexpr (LZ) {
-      // the first tile takes the exact path directly (m = -1e30 would send it there anyway, after a wasted pass)
-      bool fast = kt > 0;
-      if (fast) {
-        // against the running max, no tile max
-#pragma unroll
-        for (int qi = 0; qi < 2; ++qi) {
-          const float nm = -m[qi];
-          float a = 0.f;
-#pragma unroll
-          for (int kj = 0; kj < 4; ++kj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float e = __builtin_amdgcn_exp2f(fmaf(s[kj][qi][r], p.scale_log2, nm));
-              s[kj][qi][r] = e;
-              a += e;
-            }
-          ls[qi] = a;
-        }
-        if (__any(!(ls[0] <= LZ_TH) || !(ls[1] <= LZ_TH))) {
-          // exact path (rare past the first tile): the K fragments again from this tile's LDS image
-          fast = false;
-          bf16x8 kf2[4][2];
-#pragma unroll
-          for (int kj = 0; kj < 4; ++kj)
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) kf2[kj][kk] = rd_row(Ks, kj * 16, kk, lane);
-          scores(kf2, s, k0);
-        }
-      }
-      if (!fast) exact(s, ls);
-    } else {
-      exact(s, ls);
-    }
+    exact(s, ls);
     l[0] += ls[0];
     l[1] += ls[1];
     // O^T += V^T P^T
@@ -322,15 +271,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
         o[hj][1] = mma16<H>(vf[hj][ss], p1, o[hj][1]);
       }
     }
-    if constexpr (ST == 3) {
-      // tile kt+1 must have landed for every wave; tile kt+2 (issued this iteration) may stay in flight
-      if (kt + 2 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    // tile kt+1 must have landed for every wave; tile kt+2 (issued this iteration) may stay in flight
+    if (kt + 2 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 
   // epilogue
@@ -440,6 +384,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
       }
     }
     const int k0 = kt * KT;
+    // P recomputed with the forward's exp2 (v_exp_f32) and, on interior tiles (no key tail, no query tail, not on
+    // the causal diagonal: wave-uniform), without the per-element mask
+    const bool need_mask = (k0 + KT > p.Tk) || (qw + QW > p.Tq) || (p.causal && k0 + KT - 1 > qw + off);
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
       const int q = qw + qi * 16 + li;
@@ -448,8 +395,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = k0 + kj * 16 + 4 * g + r;
-          const bool ok = key < p.Tk && q < p.Tq && (!p.causal || key <= q + off);
-          const float pr = ok ? exp2f(s[kj][qi][r] * p.scale_log2 - lse2[qi]) : 0.f;
+          const bool ok = !need_mask || (key < p.Tk && q < p.Tq && (!p.causal || key <= q + off));
+          const float pr = ok ? __builtin_amdgcn_exp2f(s[kj][qi][r] * p.scale_log2 - lse2[qi]) : 0.f;
           s[kj][qi][r] = pr * (dp[kj][qi][r] - Dq[qi]);   // dS^T
         }
     }
@@ -483,7 +430,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
 }
 
 // dK, dV: per key block (32 keys per wave, 128 per workgroup), loop over query tiles
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnP p) {
+// Two workgroups per CU (round 4): 218 VGPRs, two waves per SIMD hide each other's LDS / exp / MFMA latencies.  At
+// one workgroup per CU (round 3: 268-276 VGPRs, accumulators shuffled through AGPRs) the encoder-shape backward
+// took 6.1 ms against 4.6 ms now (tools/bench_attn.py, same box, profiles/r04_h_attn_bwd_ab.log).
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB + 2 * 2 * 64 * 4];
   const int lane = lane_id(), wave = wave_id_uniform();
   const int g = lane >> 4, li = lane & 15;
@@ -557,6 +507,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnP p) {
         dp[qf][1] = MFMA(da, vf[1][kk], dp[qf][1]);
       }
     }
+    // interior tiles (no query tail, no key tail, not on the causal diagonal: wave-uniform) skip the mask
+    const bool need_mask = (q0 + KT > p.Tq) || (kw + QW > p.Tk) || (p.causal && kw + QW - 1 > q0 + off);
 #pragma unroll
     for (int qf = 0; qf < 4; ++qf)
 #pragma unroll
@@ -567,8 +519,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnP p) {
 #pragma unroll
         for (int kj = 0; kj < 2; ++kj) {
           const int key = kw + kj * 16 + li;
-          const bool ok = q < p.Tq && key < p.Tk && (!p.causal || key <= q + off);
-          const float pr = ok ? exp2f(s[qf][kj][r] * p.scale_log2 - l2) : 0.f;
+          const bool ok = !need_mask || (q < p.Tq && key < p.Tk && (!p.causal || key <= q + off));
+          const float pr = ok ? __builtin_amdgcn_exp2f(s[qf][kj][r] * p.scale_log2 - l2) : 0.f;
           s[qf][kj][r] = pr;                              // P
           dp[qf][kj][r] = pr * (dp[qf][kj][r] - Dq);      // dS
         }
@@ -630,24 +582,7 @@ extern "C" int tw_attn_fwd(const void* Q, int64_t ldq, const void* K, int64_t ld
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
-  static const int variant = [] {
-    // A/B benchmarking only: 0 = 16x16 kernel with the per-tile max (default), 1 = the 16x16 kernel with the
-    // lazy max (enc self 1066 -> 1033 us, cross 363 -> 349 us, tools/bench_attn.py r03, but the dominant weight
-    // of a row is then rounded too: the encoder output's share within 2 bf16 ulps of HF autocast fell below the
-    // 0.999 bound of tests/test_distill_gpu.py, so it stays opt-in), 2 = the per-tile max with the round-3
-    // 2-stage K/V ring.  (The round-2/3 32x32x16 software-pipelined kernel, no faster, was deleted in round 4.)
-    const char* e = getenv("TW_ATTN_FWD");
-    return e ? atoi(e) : 0;
-  }();
-  if (variant == 1) {
-    hipLaunchKernelGGL((attn_fwd_kernel<false, true>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
-  } else if (variant == 2) {
-    hipLaunchKernelGGL((attn_fwd_kernel<false, false, 2>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
-  } else {
-    // 3-deep K/V ring (two tiles in flight): identical arithmetic to the 2-stage ring, enc self 1108 -> 1085 us,
-    // cross 384 -> 360 us (tools/bench_attn.py, same box, round 4)
-    hipLaunchKernelGGL((attn_fwd_kernel<false, false, 3>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
-  }
+  hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
@@ -665,7 +600,7 @@ extern "C" int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
-  hipLaunchKernelGGL((attn_fwd_kernel<true, false, 3>), dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -718,13 +718,10 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   // 26.9 -> 14.6 us, B = 16 46.9 -> 31.2 us; from B = 64 (1280 pairs) the one-workgroup-per-pair kernel is
   // faster (90.6 vs 114.8 us).  With tk_dev (self-attention over a graph-captured cache) the host does
   // not know Tk, so the chunks would have to cover the kernel's DA_MAX_TK bound: measured on c5 (batch-1
-  // long-form, Tk <= 448) that costs more than it saves (2.75 -> 2.93 ms per decode step), so only
-  // TW_DECODE_SPLIT=3 (A/B) splits those.  TW_DECODE_SPLIT: 0 = never, 2 = every fixed-Tk call, else
-  // (default) fixed-Tk calls below 640 pairs.
-  static const int split_mode = [] { const char* e = getenv("TW_DECODE_SPLIT"); return e ? atoi(e) : 1; }();
-  const int nchunk = tk_dev ? DA_MAX_TK / DA_SPLIT : (Tk + DA_SPLIT - 1) / DA_SPLIT;
-  const bool split = tk_dev ? split_mode == 3 && B * H < 640
-                            : split_mode == 2 ? true : split_mode == 0 ? false : B * H < 640;
+  // long-form, Tk <= 448) that costs more than it saves (2.75 -> 2.93 ms per decode step), so only fixed-Tk calls
+  // below 640 pairs split.
+  const int nchunk = (Tk + DA_SPLIT - 1) / DA_SPLIT;
+  const bool split = !tk_dev && B * H < 640;
   if (split && nchunk >= 2 && nchunk <= DA_MAX_CHUNK) {
     float* ws = (float*)tw_device_workspace(stream, (size_t)B * H * nchunk * 66 * sizeof(float));
     if (ws) {

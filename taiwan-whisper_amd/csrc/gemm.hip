@@ -544,21 +544,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
 // Row blocks per skinny launch: batches of 65..128 rows run as 2 blocks of 64 (blockIdx.z) -- the
 // 128-row form loads 8 A fragments per W fragment and measured 18 / 31 us on the large-v2 decode
 // out_proj / fc2 at M = 128 against 14.5 / 18 us at M = 64 (tools/bench_decode_gemm.py); W is then read
-// twice, the second time from L2.  TW_SKINNY_ZSPLIT=0 keeps the single 128-row block (A/B runs).
-// TW_SKINNY_ROWS (16 / 32 / 64, A/B runs): rows per block for batches above it.
-int skinny_block_rows() {
-  static const int r = [] {
-    const char* e = getenv("TW_SKINNY_ROWS");
-    const int v = e ? atoi(e) : 64;
-    return (v == 16 || v == 32 || v == 64) ? v : 64;
-  }();
-  return r;
-}
-int skinny_row_blocks(int M) {
-  static const int env = [] { const char* e = getenv("TW_SKINNY_ZSPLIT"); return e ? atoi(e) : 1; }();
-  const int R = skinny_block_rows();
-  return (env && M > R) ? (M + R - 1) / R : 1;
-}
+// twice, the second time from L2.
+constexpr int SKINNY_ROWS = 64;
+int skinny_block_rows() { return SKINNY_ROWS; }
+int skinny_row_blocks(int M) { return M > SKINNY_ROWS ? (M + SKINNY_ROWS - 1) / SKINNY_ROWS : 1; }
 
 template <bool H>
 void launch_skinny(GemmP p, hipStream_t stream, int S = 1) {
@@ -630,15 +619,10 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
   p.tiles_total = p.tiles_mn * batch;
   int grid = p.tiles_total <= cus ? p.tiles_total : (cus & ~7);
   if (p.flags & 8192) grid = p.tiles_total;   // diagnostic: one tile per workgroup
-  // default: two 32-MFMA phases per K-tile (PRIO 4); flags bits 15-17 select the A/B variants
-  // (1: four 16-MFMA phases, per-phase priority = the previous default; 2..4 as documented above)
-  static const int env_variant = [] {
-    const char* e = getenv("TW_PP_VARIANT");   // A/B runs of whole steps only (bench.py)
-    return e ? atoi(e) : -1;
-  }();
-  // (the round-2 diagnostic variants PRIO 0/1/2/5/6/7 stay in the source but are no longer instantiated:
-  // each is a full copy of the kernel; TW_PP_DIAG_VARIANTS=1 at build time brings them back)
-  switch (env_variant >= 0 ? env_variant : (p.flags >> 15) & 7) {
+  // default: two 32-MFMA phases per K-tile (PRIO 4); flags bits 15-17 select the diagnostic variants
+  // (the round-2 variants PRIO 0/1/2/5/6/7 stay in the source but are instantiated only in a diagnostic build:
+  // each is a full copy of the kernel; -DTW_PP_DIAG_VARIANTS brings them back, tools/bench_pp_prio.py)
+  switch ((p.flags >> 15) & 7) {
 #ifdef TW_PP_DIAG_VARIANTS
     case 1: hipLaunchKernelGGL((gemm_pp_kernel<H, 0>), dim3(grid), dim3(512), 0, stream, p); break;
     case 2: hipLaunchKernelGGL((gemm_pp_kernel<H, 2>), dim3(grid), dim3(512), 0, stream, p); break;
@@ -900,23 +884,12 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   p.res = res; p.ldr = ldr; p.sR = sR; p.res_dtype = res_dtype; p.res_mod = res_mod;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux; p.c_dtype = c_dtype; p.flags = flags;
   p.ws = nullptr;
-  static const int env_group = [] {
-    const char* e = getenv("TW_GEMM_GROUP_M");   // A/B sweeps only (tools/bench_gemm.py)
-    return e ? atoi(e) : 0;
-  }();
   // tile order: runs of 8 m-tiles walked n-tile by n-tile for the tall, short-K forward GEMMs (the
   // encoder's M = B x 1500 projections: +3-5 % from L2 reuse of the weight panels,
   // tools/bench_pp_prio.py with TW_GEMM_GROUP_M); plain row-major elsewhere (K = 5120 and the
-  // decoder's M = B x 447 shapes lose with grouping)
+  // decoder's M = B x 447 shapes lose with grouping: round 4, profiles/r04_b_l2_epilogue_study.txt)
   const bool grouped = !a_trans && !b_trans && batch == 1 && M >= 65536 && K <= 2048;
-  // TW_GEMM_GROUP_DEC (A/B): runs of that many m-tiles for the decoder's mid-width projections (M < 65536,
-  // 2048 <= N <= 4096: the teacher's fused QKV measured 1025 -> 1119 TF/s with runs of 2, tools/gemm_own_shapes.sh)
-  static const int env_group_dec = [] {
-    const char* e = getenv("TW_GEMM_GROUP_DEC");
-    return e ? atoi(e) : 0;
-  }();
-  const bool dec_mid = !a_trans && !b_trans && batch == 1 && M < 65536 && N >= 2048 && N <= 4096 && K <= 2048;
-  p.group_m = env_group > 0 ? env_group : (grouped ? 8 : (dec_mid && env_group_dec > 0 ? env_group_dec : 1));
+  p.group_m = grouped ? 8 : 1;
   if ((flags >> 24) & 15) p.group_m = (flags >> 24) & 15;     // forced tile order (A/B runs: tools/bench_group.py)
   p.epi = pick_epilogue(p, batch);
   // 256x256 tiles (8 waves) when the problem has enough tiles to fill the chip, else 128x128
@@ -932,14 +905,10 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   // K-major forward grids of 1-4 rounds whose rounds are well filled (c2's B = 32 shapes: the teacher encoder's
   // N = 1280 Linears at M = 48 000, 940 256-tiles = 3.67 rounds, 92 % of the workgroup-rounds busy; the student
   // decoder's fused QKV and fc1): the persistent kernel.  Grids with a mostly idle last round take the whole-round
-  // + 128x128 tail split below (dp_tail_plan).  TW_PP_MINFILL (percent, A/B runs): the fill threshold.
-  static const int env_minfill = [] {
-    const char* e = getenv("TW_PP_MINFILL");
-    return e ? atoi(e) : 85;
-  }();
-  if (!a_trans && !b_trans && tile == 128 && K >= 256 && env_minfill <= 100) {
+  // + 128x128 tail split below (dp_tail_plan).  Fill threshold 85 % (c2 +0.6 %, c3 unchanged: same box, round 4)
+  if (!a_trans && !b_trans && tile == 128 && K >= 256) {
     const int64_t G = pp_grid_cus();
-    if (t256 >= G && t256 * 100 >= ((t256 + G - 1) / G) * G * env_minfill) tile = 256;
+    if (t256 >= G && t256 * 100 >= ((t256 + G - 1) / G) * G * 85) tile = 256;
   }
   if (tile == 256 && !a_trans && !b_trans) tile = 2562;
   if (flags & 256) tile = 128;        // forced tile (benchmarking / A-B comparisons)
@@ -953,11 +922,9 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
   // decode-step GEMMs (tools/bench_skinny.py, r01): the weight-streaming kernel wins for N <= 3840
   // (and N <= 8192 at M <= 64); the LM head and wide M=128 GEMMs stream faster as 128x128 tiles
-  // TW_SKINNY_MAXM (A/B runs): row-blocked skinny launches above 128 rows too.  Measured at M = 512
-  // (tools/bench_decode_gemm.py): qkv 50 vs 21 us, fc2 69 vs 60 us against the 128x128 tiles, so 128 stays.
-  static const int skinny_max_m = [] { const char* e = getenv("TW_SKINNY_MAXM"); return e ? atoi(e) : 128; }();
-  const int max_m = skinny_row_blocks(M) > 1 ? std::max(128, skinny_max_m) : 128;
-  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= max_m && (N <= 4096 || (M <= 64 && N <= 8192)) &&
+  // (row-blocked skinny launches above 128 rows measured slower at M = 512, tools/bench_decode_gemm.py: qkv 50 vs
+  // 21 us, fc2 69 vs 60 us against the 128x128 tiles)
+  const bool skinny = !a_trans && !b_trans && batch == 1 && M <= 128 && (N <= 4096 || (M <= 64 && N <= 8192)) &&
                       !(flags & (256 | 512 | 1024 | 2048));
   if (skinny && ((uintptr_t)A & 15) == 0) {
     // decode-step GEMMs: stream W once.  With fewer than 512 workgroups and M > 32 the K range is
@@ -1006,22 +973,12 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     }
   }
   // mid-sized forward grids (1-4 rounds of 256-tiles): whole rounds persistent + a split-K tail
-  // (TW_GEMM_SK=0 disables it for A/B runs; flag 262144 forces the 256x128 2-stage tile)
-  static const int env_sk = [] {
-    const char* e = getenv("TW_GEMM_SK");
-    return e ? atoi(e) : 1;
-  }();
+  // (flag 262144 forces the 256x128 2-stage tile)
   if (flags & 262144) tile = 2563;
   // (tools/bench_gemm_dec.py: fc2 K = 5120 417 -> 347 us; at K = 1280 the split's fp32 round trip costs
-  // more than the third round it saves, 125 -> 140 us, so short K stays on the 128x128 kernel)
-  // TW_GEMM_SK_SUB_MINK (A/B): the shortest K for which grids of less than one round of 256-tiles (the 512-clip
-  // decode step's Linears) are split over K on the persistent kernel; whole-round + tail splits keep K >= 3072
-  static const int env_sk_sub_mink = [] {
-    const char* e = getenv("TW_GEMM_SK_SUB_MINK");
-    return e ? atoi(e) : 3072;
-  }();
-  const bool sub_round = (int64_t)((M + 255) / 256) * ((N + 255) / 256) < pp_grid_cus() && M >= 256;
-  if (!a_trans && !b_trans && tile == 128 && env_sk && (K >= 3072 || (sub_round && K >= env_sk_sub_mink)) &&
+  // more than the third round it saves, 125 -> 140 us, so short K stays on the 128x128 kernel; grids of less than
+  // one round, the 512-clip decode step's Linears, follow the same K >= 3072 rule)
+  if (!a_trans && !b_trans && tile == 128 && K >= 3072 &&
       !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
     int m_dp = 0;
     const int S = sk_tail_plan(p, batch, m_dp);
@@ -1029,12 +986,8 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     const bool full = !H || ((N % 256) == 0 && ((M - m_dp * 256) % 256) == 0 && p.epi != EPI_GENERIC);
     if (S > 0 && full && launch_sk_tail<H>(p, S, m_dp, stream)) return TW_OK;
   }
-  // whole rounds persistent + a 128x128 tail (dp_tail_plan); TW_GEMM_DPTAIL=0 disables it (A/B runs)
-  static const int env_dpt = [] {
-    const char* e = getenv("TW_GEMM_DPTAIL");
-    return e ? atoi(e) : 1;
-  }();
-  if (!a_trans && !b_trans && env_dpt && !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
+  // whole rounds persistent + a 128x128 tail (dp_tail_plan)
+  if (!a_trans && !b_trans && !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
     int m_dp = 0;
     // (fp16: the persistent part must be whole 256x256 tiles with a fast epilogue)
     if (dp_tail_plan(p, batch, m_dp) && (!H || ((N % 256) == 0 && p.epi != EPI_GENERIC)) &&
@@ -1044,12 +997,8 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   // Grids of at most one 128x128 tile per CU (the 512-clip decode step's Linears: 40-160 tiles, one workgroup per
   // CU anyway) run on a 4-stage ring: three K-steps in flight instead of one hide the load latency that bounds a
   // 20-K-step tile.  Same tile, same K order: bit-identical.  c4 fp16 155.8 -> 158.5 utt/s, c5 16.93 -> 17.09
-  // audio s/s (same box, profiles/r03_s_gemm_deep_ab.log).  TW_GEMM_DEEP=0: the 2-stage kernel (A/B runs).
-  static const int env_deep = [] {
-    const char* e = getenv("TW_GEMM_DEEP");
-    return e ? atoi(e) : 1;
-  }();
-  if (env_deep && tile == 128 && !a_trans && !b_trans && !(flags & 256) &&
+  // audio s/s (same box, profiles/r03_s_gemm_deep_ab.log).  Flag 256 (forced 128x128) keeps the 2-stage kernel.
+  if (tile == 128 && !a_trans && !b_trans && !(flags & 256) &&
       (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch <= pp_grid_cus())
     tile = 1284;
   if constexpr (H) {
