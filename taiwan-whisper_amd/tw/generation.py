@@ -328,6 +328,130 @@ class _Decoder:
         return gen[:, :L]
 
 
+class _BeamDecoder:
+    """Beam search over B clips x k beams with the same prompt (short-form, no timestamps): HF
+    GenerationMixin._beam_search (transformers 5.15 generation/utils.py:3208-3560), the search behind
+    `training/run_eval.py:144-147` (--num_beams) and `run_distillation.py:1476-1484` (generation_num_beams).
+    The B*k rows decode as one batch on the engine's step (DecodeSession, every clip's encoder rows repeated k
+    times); per step, on the device: fp32 log-softmax of the logits, the suppress processors on the log-probs,
+    plus the running scores, the top 2k of k*V candidates, the k best unfinished continue (the self-attention
+    caches gathered by their source beams), finished candidates among the top k enter the per-clip set of k
+    hypotheses with score sum(log p) / generated_length ** length_penalty; the search stops when no running beam
+    can beat the worst kept hypothesis (early_stopping False: the heuristic at the current length) or every
+    candidate hits max_length."""
+
+    def __init__(self, model, gc, B, nb, Tk, P, max_length):
+        self.m, self.gc, self.B, self.nb, self.Tk, self.P, self.T_max = model, gc, B, nb, Tk, P, max_length
+        dev = model.device
+        self.V = model.config.vocab_size
+        self.eos = int(gc.eos_token_id)
+        pad = getattr(gc, "pad_token_id", None)
+        self.fill = int(pad) if pad is not None else self.eos
+        self.sup = torch.tensor(sorted(set(gc.suppress_tokens or [])), dtype=torch.int64, device=dev)
+        self.beg = torch.tensor(sorted(set(gc.begin_suppress_tokens or [])), dtype=torch.int64, device=dev)
+        self.length_penalty = float(getattr(gc, "length_penalty", 1.0) if getattr(gc, "length_penalty", None)
+                                    is not None else 1.0)
+        es = getattr(gc, "early_stopping", False)
+        self.early_stopping = False if es is None else es
+
+    @staticmethod
+    def _gather(t, idx):
+        """HF _gather_beams: t [B, K, ...] rows picked per clip by idx [B, k]."""
+        while idx.dim() < t.dim():
+            idx = idx.unsqueeze(-1)
+        return torch.gather(t, 1, idx.expand(*idx.shape[:2], *t.shape[2:]))
+
+    def run(self, enc16, prompt):
+        """enc16: [B*Tk, d] encoder rows; prompt: int64 [P] (device or host) -> generated ids [B, L] (device)."""
+        m, B, nb, P, T_max, V = self.m, self.B, self.nb, self.P, self.T_max, self.V
+        dev = m.device
+        d = m.config.d_model
+        BN = B * nb
+        prompt = torch.as_tensor(prompt, dtype=torch.int64, device=dev)
+        enc_rep = enc16.view(B, self.Tk, d).repeat_interleave(nb, 0).reshape(BN * self.Tk, d).contiguous()
+        sess = DecodeSession(m, enc_rep, BN, self.Tk, T_max)
+        del enc_rep
+        sess.t_dev.zero_()
+        for t in range(P - 1):                                   # prompt prefill (identical on every row)
+            sess.cur.fill_(int(prompt[t]))
+            sess.step()
+        sess.cur.fill_(int(prompt[P - 1]))
+        K = max(2, 2) * nb                                       # beams_to_keep: (1 eos token + 1) * k
+        top_mask = torch.zeros(K, dtype=torch.bool, device=dev)
+        top_mask[:nb] = True
+        run_seq = torch.full((B, nb, T_max), self.fill, dtype=torch.int64, device=dev)
+        run_seq[:, :, :P] = prompt
+        seqs = run_seq.clone()
+        run_scores = torch.zeros(B, nb, dtype=torch.float32, device=dev)
+        run_scores[:, 1:] = -1e9
+        scores = torch.full((B, nb), -1e9, dtype=torch.float32, device=dev)
+        finished = torch.zeros(B, nb, dtype=torch.bool, device=dev)
+        heur_unsat = torch.ones(B, 1, dtype=torch.bool, device=dev)
+        run_bidx = torch.full((B, nb, T_max - P), -1, dtype=torch.int32, device=dev)
+        bidx = run_bidx.clone()
+        lp, es = self.length_penalty, self.early_stopping
+        cur = P
+        while True:
+            sess.step()                                          # logits of position cur - 1 on every row
+            logp = torch.log_softmax(sess.logits[:, :V].float(), dim=-1)
+            if self.sup.numel():
+                logp[:, self.sup] = -float("inf")
+            if cur == P and self.beg.numel():                    # SuppressTokensAtBegin (begin_index = P)
+                logp[:, self.beg] = -float("inf")
+            acc = (logp.view(B, nb, V) + run_scores[:, :, None]).reshape(B, nb * V)
+            # _get_top_k_continuations
+            top_lp, top_i = torch.topk(acc, k=K)
+            src = top_i // V
+            tok = top_i % V
+            top_bidx = self._gather(run_bidx, src)
+            top_seq = self._gather(run_seq, src)
+            top_seq[:, :, cur] = tok
+            top_bidx[:, :, cur - P] = (src + torch.arange(B, device=dev).view(-1, 1) * nb).to(torch.int32)
+            # stopping criteria on each candidate: eos, or the sequence reaching max_length
+            hits = (tok == self.eos) | (cur + 1 >= T_max)
+            # _get_running_beams_for_next_iteration
+            run_lp = top_lp + hits.to(torch.float32) * -1.0e9
+            nxt = torch.topk(run_lp, k=nb)[1]
+            run_seq = self._gather(top_seq, nxt)
+            run_scores = self._gather(run_lp, nxt)
+            run_bidx = self._gather(top_bidx, nxt)
+            # _update_finished_beams
+            just = hits & top_mask[None, :]
+            fin_lp = top_lp / ((cur + 1 - P) ** lp)
+            full = torch.all(finished, dim=-1, keepdim=True) & (es is True)
+            fin_lp = fin_lp + full.to(torch.float32) * -1.0e9
+            fin_lp = fin_lp + (~heur_unsat).to(torch.float32) * -1.0e9
+            fin_lp = fin_lp + (~just).to(torch.float32) * -1.0e9
+            m_seq = torch.cat((seqs, top_seq), 1)
+            m_sc = torch.cat((scores, fin_lp), 1)
+            m_bi = torch.cat((bidx, top_bidx), 1)
+            m_fin = torch.cat((finished, just), 1)
+            keep = torch.topk(m_sc, k=nb)[1]
+            seqs, scores = self._gather(m_seq, keep), self._gather(m_sc, keep)
+            bidx, finished = self._gather(m_bi, keep), self._gather(m_fin, keep)
+            # the next step's inputs: caches gathered by each running beam's source row, its new token
+            src_rows = run_bidx[:, :, cur - P].reshape(-1).to(torch.int64)
+            for c in sess.self_kv:
+                c[:, :cur].copy_(c[:, :cur].index_select(0, src_rows))
+            sess.cur.copy_(run_seq[:, :, cur].reshape(-1))
+            cur += 1
+            # _check_early_stop_heuristic / _beam_search_has_unfinished_sequences
+            if es == "never" and lp > 0.0:
+                best_len = T_max - P
+            else:
+                best_len = cur - P
+            best_run = run_scores[:, :1] / (best_len ** lp)
+            worst_fin = torch.where(finished, torch.min(scores, dim=1, keepdim=True)[0], torch.full_like(scores, -1e9))
+            heur_unsat = heur_unsat & torch.any(best_run > worst_fin, dim=-1, keepdim=True)
+            go = bool(torch.any(heur_unsat)) and not (bool(torch.all(finished)) and es is True) and \
+                not bool(torch.all(hits))
+            if not go or cur >= T_max:
+                break
+        best = seqs[:, 0]
+        gen_len = int(((bidx[:, 0] + 1) != 0).sum(dim=1).max())
+        return best[:, P:P + gen_len]
+
+
 def total_length(cfg, gc, P, max_length=None, max_new_tokens=None):
     """Length cap of prompt + generated tokens, HF _set_max_new_tokens_and_length
     (generation_whisper.py:1919-1945): max_new_tokens counts after the P prompt tokens; a max_length
@@ -367,8 +491,11 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
              task=None, decoder_input_ids=None, max_new_tokens=None, encoder_outputs=None, attention_mask=None,
              use_graph=None, **kw):
     from .config import GenerationConfig
-    if num_beams not in (None, 1):
-        raise NotImplementedError("tw generate: greedy only (num_beams=1, as every reference call site)")
+    nb = 1 if num_beams is None else int(num_beams)
+    if nb > 1 and (return_timestamps or (input_features is not None and input_features.shape[-1] >
+                                          2 * model.config.max_source_positions)):
+        raise NotImplementedError("tw generate: beam search is built for short-form decoding without timestamps "
+                                  "(run_eval.py --num_beams / generation_num_beams at the reference's defaults)")
     temperature = kw.get("temperature")
     fb = dict(temperature=temperature if temperature is not None else 0.0,
               compression_ratio_threshold=kw.get("compression_ratio_threshold"),
@@ -413,6 +540,10 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     max_length = total_length(cfg, gc, P, max_length, max_new_tokens)
     if P >= max_length:
         return torch.empty(B, 0, dtype=torch.int64, device=model.device)
+    if nb > 1:
+        if not bool((prompt == prompt[:1]).all()):
+            raise NotImplementedError("tw generate: beam search takes one prompt for every clip")
+        return _BeamDecoder(model, gc, B, nb, Tk, P, max_length).run(enc16, prompt[0])
     dec = _Decoder(model, gc, B, Tk, P, max_length, bool(return_timestamps), use_graph)
     if kw.get("_keep") is not None:          # tests: the decoder (and its device caches) outlive the call
         kw["_keep"].append(dec)

@@ -676,7 +676,7 @@ class WhisperForConditionalGeneration:
     forward = __call__
 
     def generate(self, input_features=None, **kw):
-        """Greedy decoding with a KV cache (tw/generation.py)."""
+        """Greedy (or, num_beams > 1, beam-search) decoding with a KV cache (tw/generation.py)."""
         from .generation import generate
         return generate(self, input_features, **kw)
 

@@ -240,6 +240,36 @@ def gen_greedy(out):
     out["suppress"] = np.array(SUPPRESS)
 
 
+def gen_beam(out):
+    """HF `generate(num_beams=k)` (short-form, forced prompt, no timestamps) on the greedy fixture's model and clips:
+    the beam search of `training/run_eval.py:144-147` / `run_distillation.py:1476-1484` (GenerationMixin._beam_search:
+    log-softmax, the suppress processors on log-probs, 2k candidates, length penalty 1.0, early_stopping False).
+    Two weight sets: the greedy fixture's (every beam runs to max_length) and the same with the <|endoftext|> row of the
+    tied embedding scaled by 6 (beams finish at different steps: the finished-hypotheses path)."""
+    from transformers import GenerationConfig
+    cfg = CONFIGS["micro"]
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0),
+                                                   logmel.synthetic_clip(4, 25.0)]))
+    prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
+    for tag, eos_scale in (("", 1.0), ("_eos6", 6.0)):
+        w = make_weights(cfg, 1, lin_std=0.2)
+        w["model.decoder.embed_tokens.weight"] = w["model.decoder.embed_tokens.weight"].copy()
+        w["model.decoder.embed_tokens.weight"][SPECIAL["eot"]] *= eos_scale
+        m = hf_model(cfg, w).eval()
+        for nb in (2, 4):
+            gc = GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
+                                  pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
+                                  begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=64, num_beams=nb,
+                                  do_sample=False, no_timestamps_token_id=SPECIAL["notimestamps"])
+            m.generation_config = gc
+            with torch.no_grad():
+                ids = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * 3), max_length=64, num_beams=nb,
+                                 do_sample=False)
+            out[f"beam{nb}{tag}_ids"] = ids.numpy()      # generated tokens only, finished rows padded with eos
+    out["beam_prompt"] = np.array(prompt)
+    out["beam_eos_scale"] = np.float32(6.0)
+
+
 def ts_generation_config():
     from transformers import GenerationConfig
     return GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
@@ -606,7 +636,7 @@ def gen_cfg(case, out):
 def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
-    for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy),
+    for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy), ("beam", gen_beam),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
                      ("lv2_decode", gen_lv2_decode),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
