@@ -166,6 +166,32 @@ __device__ __forceinline__ void pp_stage(const bf16* base, int64_t ld, int rows_
   }
 }
 
+// The same for a whole 64-deep K-tile (every k valid): the lane part of the source offset is loop-invariant -- piece
+// row (lane >> 3), 16-B chunk (lane & 7) ^ (lane >> 3), since a piece's first region row is a multiple of 8 -- so it
+// is computed once per kernel (`lane_off`); the piece's row adds one scalar term and the K-tile goes into the scalar
+// offset.  Rows past the operand (a ragged last tile) read zeros through the descriptor's bound (`bytes` = the
+// valid rows x ld from the tile base; the K offset never leaves a valid row), so there is no per-lane compare (the
+// checked form's row / bound arithmetic ran in the load segments, beside the partner wave's MFMAs).
+__device__ __forceinline__ uint32_t pp_lane_off(int64_t ld, int lane) {
+  const int r = lane >> 3;
+  return (uint32_t)(((int64_t)r * ld + ((lane & 7) ^ r) * 8) * 2);
+}
+template <int S, int GS>
+__device__ __forceinline__ void pp_stage_full(const bf16* base, int64_t ld, int rows_left, uint32_t lane_off, int kt,
+                                              int off, char* region, int wave) {
+  // (only this tile's 256 rows are ever addressed: the bound stays 32-bit, <= 256 x ld x 2 bytes)
+  const int bytes = rows_left > 0 ? (rows_left < 256 ? rows_left : 256) * (int)ld * 2 : 0;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pce = wave + 8 * i;
+    const int R0 = pce * 8;
+    const int row0 = (R0 >> S) * GS + off + (R0 & ((1 << S) - 1));
+    const uint32_t voff = lane_off + (uint32_t)(row0 * (int)ld * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + pce * 1024), 16, voff, (uint32_t)(kt * BK * 2), 0, 0);
+  }
+}
+
 // Epilogue of fragment rows MI0 .. MI1-1 of finished tile `ti` of this workgroup, then those accumulators
 // are zeroed for the next tile.  Debug flags: 4096 skips the stores, 1 << 20 stores every tile to tile 0.
 template <bool H, int KIND, int MI0, int MI1>
@@ -194,7 +220,9 @@ __device__ __forceinline__ void pp_epi_part(const GemmP& p, f32x4 (&acc)[8][4], 
 // prio 1 around each MFMA phase; 1 = the same with static prio 1 for the trailing wave row
 // (waves 4-7), no flips; 2 = diagnostic: every MFMA phase issued twice (wrong results; measures
 // the fixed per-phase cost); 4 = two 32-MFMA phases per K-tile (default: +4-8 % main loop)
-template <bool H, int PRIO, int KIND = -1>
+// KF: K is a multiple of 64 (every launch of the model's shapes but the conv stem's K = 240): staging without per-lane
+// bound arithmetic (pp_stage_full).  KF = false keeps the checked stager for a K tail (generic epilogue only).
+template <bool H, int PRIO, int KIND = -1, bool KF = true>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   // + 2 x 1 KiB: the bias slice of the current tile (by tile parity), for the fast epilogue (one array:
   // a second __shared__ object can make the compiler drain vmcnt before LDS reads)
@@ -224,6 +252,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   auto tile_info = [&](int i, const bf16*& pa, const bf16*& pb, int& rows, int& cols, int& kl) {
     int m0 = 0, n0 = 0, bz = 0;
     const bool live = i < my_tiles && pp_tile(p, i, m0, n0, bz);
+#ifdef TW_PP_DIAG_VARIANTS
+    // diagnostic build only, flag 1 << 22: every tile stages the panels of its workgroup's XCD-first tile (A rows and
+    // B columns of one 256 x 256 block per XCD, L2-resident): the main loop without L2 misses (wrong results)
+    if (p.flags & (1 << 22)) { m0 = p.M >= 2048 ? ((int)blockIdx.x & 7) * 256 : 0; n0 = 0; bz = 0; }
+#endif
     pa = p.A + bz * p.sA + (int64_t)m0 * p.lda;
     pb = p.B + bz * p.sB + (int64_t)n0 * p.ldb;
     rows = p.M - m0;
@@ -231,12 +264,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
     kl = live ? K : 0;
   };
   auto reg = [&](int b, int r) -> char* { return smem + (b * 4 + r) * PP_REGION; };
+  const uint32_t lane_off_a = KF ? pp_lane_off(p.lda, lane) : 0u, lane_off_b = KF ? pp_lane_off(p.ldb, lane) : 0u;
   auto stage = [&](const bf16* pa, const bf16* pb, int rows, int cols, int kl, int kt, int buf, int r) {
     const int k_left = kl - kt * BK;
-    if (r < 2)
-      pp_stage<6, 128>(pa + kt * BK, p.lda, rows, k_left, r * 64, reg(buf, r), wave, lane);
-    else
-      pp_stage<5, 64>(pb + kt * BK, p.ldb, cols, k_left, (r - 2) * 32, reg(buf, r), wave, lane);
+    if constexpr (KF) {
+      // a whole K-tile, or none (a dead tile or the pad K-tile: k_left <= 0 -> zero valid rows -> zeros)
+      const int valid = k_left > 0 ? 1 : 0;
+      if (r < 2) pp_stage_full<6, 128>(pa, p.lda, rows * valid, lane_off_a, kt, r * 64, reg(buf, r), wave);
+      else pp_stage_full<5, 64>(pb, p.ldb, cols * valid, lane_off_b, kt, (r - 2) * 32, reg(buf, r), wave);
+    } else {
+      if (r < 2) pp_stage<6, 128>(pa + kt * BK, p.lda, rows, k_left, r * 64, reg(buf, r), wave, lane);
+      else pp_stage<5, 64>(pb + kt * BK, p.ldb, cols, k_left, (r - 2) * 32, reg(buf, r), wave, lane);
+    }
   };
 
   // PRIO 6: diagnostic, no restaging in the main loop (timing of everything but the DMA)
@@ -595,6 +634,10 @@ int pick_epilogue(const GemmP& p, int batch) {
 // ragged tiles per kernel: the split epilogue's three inlined parts stay within the register budget)
 template <bool H, int PRIO>
 void launch_pp_kind(const GemmP& p, int grid, hipStream_t stream) {
+  if (p.K % BK) {     // a K tail (the conv stem's K = 240): the checked stager with the generic epilogue
+    hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_GENERIC, false>), dim3(grid), dim3(512), 0, stream, p);
+    return;
+  }
   switch (p.epi) {
     case EPI_STORE_BF16: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_STORE_BF16>), dim3(grid), dim3(512), 0, stream, p); break;
     case EPI_STORE_F32: hipLaunchKernelGGL((gemm_pp_kernel<H, PRIO, EPI_STORE_F32>), dim3(grid), dim3(512), 0, stream, p); break;
@@ -917,7 +960,7 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (flags & 2048) tile = 2562;      // 256x256 ping-pong (K-major A and B only)
   // the fp16 persistent kernel is compiled with the fast full-tile epilogues only (gemm_impl.h epilogue_k):
   // ragged shapes and the generic epilogue kind take the 128x128 kernel
-  if (H && tile == 2562 && ((M % 256) || (N % 256) || p.epi == EPI_GENERIC)) tile = 128;
+  if (H && tile == 2562 && ((M % 256) || (N % 256) || (K % BK) || p.epi == EPI_GENERIC)) tile = 128;
   const int64_t ntiles = (tile == 256 || tile == 2562) ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
   // decode-step GEMMs (tools/bench_skinny.py, r01): the weight-streaming kernel wins for N <= 3840

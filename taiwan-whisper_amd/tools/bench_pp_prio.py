@@ -15,8 +15,10 @@ SHAPES = [("enc qkv", 96000, 3840, 1280, 0), ("enc out", 96000, 1280, 1280, 0), 
           ("enc fc2", 96000, 1280, 5120, 0), ("xattn kv", 96000, 2560, 1280, 0), ("dec fc1", 28608, 5120, 1280, 1),
           ("lm head", 28608, 51904, 1280, 0)]
 VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "p4,p0,p4e").split(",")
+DT = torch.float16 if "fp16" in sys.argv[2:] else torch.bfloat16     # `... p4 fp16`: the fp16 instantiation
 FLAG = {"p4": 0, "p4e": 4096, "p4z": 1 << 20, "p4s": 1 << 21, "p0": 1 << 15, "p0e": (1 << 15) | 4096,
-        "p2x": 2 << 15, "p2xe": (2 << 15) | 4096, "p1": 3 << 15, "p5e": (5 << 15) | 4096, "p6e": (6 << 15) | 4096, "p7e": (7 << 15) | 4096}
+        "p2x": 2 << 15, "p2xe": (2 << 15) | 4096, "p1": 3 << 15, "p5e": (5 << 15) | 4096, "p6e": (6 << 15) | 4096, "p7e": (7 << 15) | 4096,
+        "p4l": 1 << 22, "p4le": (1 << 22) | 4096}     # p4l*: diagnostic build, panels of one block per XCD (L2 hits)
 
 
 def vflag(v):
@@ -26,10 +28,10 @@ def vflag(v):
 def main(rounds=5):
     dev = "cuda"
     for name, M, N, K, gelu in SHAPES:
-        A = torch.randn(M, K, device=dev).bfloat16()
-        W = torch.randn(N, K, device=dev).bfloat16()
-        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        bias = torch.randn(N, device=dev).bfloat16()
+        A = torch.randn(M, K, device=dev).to(DT)
+        W = torch.randn(N, K, device=dev).to(DT)
+        C = torch.empty(M, N, dtype=DT, device=dev)
+        bias = torch.randn(N, device=dev).to(DT)
         base = ops.GEMM_ROUND
 
         def run(v):
