@@ -391,10 +391,12 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
       }
     }
   }
-  // Residual operands are loaded a batch of row blocks at a time (2: 16 / 32 VGPRs within the budget),
-  // before any store of those rows (in-place updates): one memory round trip per batch instead of one per
-  // row block (each load waits for everything issued before it, LDS-DMA included).
-  constexpr int RB = KIND == EPI_RES_BF16 ? 2 : (KIND == EPI_RES_F32 ? 2 : 1);
+  // Residual operands are loaded a batch of row blocks at a time, before any store of those rows (in-place
+  // updates): one memory round trip per batch instead of one per row block (each load waits for everything issued
+  // before it, LDS-DMA and the previous batch's stores included).  bf16: 4 row blocks (32 VGPRs, two round trips per
+  // tile; round 4: encoder-shape out_proj 352 -> 332 us, fc1-shaped 1240 -> 1204 us, profiles/r04_l_res_epilogue_ab.log;
+  // 8 spill); fp32: 2 (32 VGPRs).
+  constexpr int RB = KIND == EPI_RES_BF16 ? 4 : (KIND == EPI_RES_F32 ? 2 : 1);
 #pragma unroll
   for (int mb = MI0; mb < FM; mb += RB) {
   u32x4 rball[KIND == EPI_RES_BF16 ? RB : 1][FN / 2];

@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round 4, call I: the working tree's GPU suite, own GEMM vs hipBLASLt (torch.matmul) on the step's shapes, then the
-# round's evidence: PMC traffic passes + kernel trace + bench line (profile_round.sh) and the MFMA-busy passes
-# (pmc_mfma.sh).  Every GPU step has its own limit; the first failure ends the call.
+# round's evidence: PMC traffic passes + kernel trace + bench line (profile_round.sh).  Every GPU step has its own limit; the first failure ends the call.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
@@ -11,4 +10,3 @@ rc=$?; grep -E "passed|failed|FAILED|Error" gpurun_out/r4i_gpu_tests.txt | tail 
 timeout -k 10 300 python -u taiwan-whisper_amd/tools/bench_vendor.py > gpurun_out/r4i_vendor.txt 2>&1 || exit 1
 grep "^gemm" gpurun_out/r4i_vendor.txt
 bash taiwan-whisper_amd/tools/profile_round.sh r04 || exit 1
-bash taiwan-whisper_amd/tools/pmc_mfma.sh || exit 1
