@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4, call N: the student's dX products on the forward route (transposed W copy) -- training-path GPU tests, then
-# same-box c2 / c3 lines against a copy of the tree with the previous tw/modeling.py (ab/modeling_base.py).
+# same-box c2 / c3 lines against a copy of the tree with the previous tw/modeling.py (ab/modeling_base.py).  Rerun
+# for the selective route (plain-epilogue products only).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out

@@ -716,11 +716,23 @@ class Backward:
                flags=F.GEMM_ROUND | F.GEMM_ACCUM)
 
     # dX[M][K] = op(g[M][N] W[N][K])
+    # Training-sized products with the plain rounding epilogue (16-bit operands, M >= 4096, no accumulate / GELU
+    # derivative) transpose W into a K-major copy first and take the forward route (persistent 256² kernel / whole-
+    # round + tail split): W is read and written once more (7-33 us) and the product runs 3-23 % faster
+    # (tools/bench_dx.py: whisper-small encoder QKV dX 248 -> 192 us, distil-32-2 decoder fc1 446 -> 378 us;
+    # profiles/r04_m_dx_route.log).  The accumulating and GELU-derivative products keep the transposed-operand kernel:
+    # on the forward route they run the persistent kernel's generic epilogue, and routing every dX measured c2 -0.8 %
+    # (profiles/r04_n_dx_route_step_ab.log).  The fp32 compute path keeps the transposed-operand form.
     def dX(self, g, w, out, flags=F.GEMM_ROUND, aux=None, M=None):
         M = g.shape[0] if M is None else M
         N, K = w.shape
-        F.gemm(g, w, out, M, K, N, lda=g.stride(0), ldb=K, ldc=out.stride(0), b_trans=True, aux=aux,
-               ldaux=aux.stride(0) if aux is not None else 0, flags=flags)
+        if (M >= 4096 and flags == F.GEMM_ROUND and aux is None and w.dtype == torch.bfloat16 and g.dtype == w.dtype
+                and out.dtype == torch.bfloat16):
+            wt = F.transpose_bf16(w, torch.empty(K, N, dtype=torch.bfloat16, device=self.dev))
+            F.gemm(g, wt, out, M, K, N, lda=g.stride(0), ldb=N, ldc=out.stride(0), flags=flags)
+        else:
+            F.gemm(g, w, out, M, K, N, lda=g.stride(0), ldb=K, ldc=out.stride(0), b_trans=True, aux=aux,
+                   ldaux=aux.stride(0) if aux is not None else 0, flags=flags)
         return out
 
     def db(self, g, cols_slice, out):
