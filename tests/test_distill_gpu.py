@@ -9,7 +9,7 @@ reference's train_step under CUDA bf16 autocast with the same rounding points as
     the reference's own autocast-vs-fp32 distance (HF under CPU bf16 autocast vs HF fp32, both in the
     micro_step fixture);
   * per-parameter gradients: relative L2 error <= 6e-3 (2e-2 for the one worst tensor, the final LN
-    bias) and cosine >= 0.9999 (bf16 GEMM outputs and
+    bias) and cosine >= 0.9999 (0.9998 for that tensor: cos ~ 1 - rel^2 / 2) (bf16 GEMM outputs and
     bf16 flash-attention probabilities round at the same points but accumulate in a different
     order, so individual bf16 elements may differ by one ulp);
   * AdamW-updated parameters: <= 2e-3 relative L2 of the update.
@@ -142,7 +142,9 @@ def test_train_step_matches_oracle(freeze_encoder):
     # least accurate; every other tensor is within 6e-3
     assert worst[0][0] < 2e-2, worst[:3]
     assert worst[1][0] < 6e-3, worst[:3]
-    assert min(w[1] for w in worst) > 0.9999, sorted(worst, key=lambda x: x[1])[:3]
+    # cosine >= 0.9999 for every gradient but that one (cos ~ 1 - rel^2 / 2: its 2e-2 bound allows 0.9998)
+    assert worst[0][1] > 0.9998, worst[:3]
+    assert min(w[1] for w in worst[1:]) > 0.9999, sorted(worst[1:], key=lambda x: x[1])[:3]
     # second micro-step with the same batch -> optimizer update with the accumulated grads
     tr.train_step(batch)        # two halves of the same batch == one full-batch gradient
     check = ("model.decoder.layers.0.fc1.weight", "model.decoder.embed_tokens.weight",
