@@ -267,7 +267,7 @@ def run_decode(args, device, rank, world, pg):
             achieved = ks["rate"] / 1e9
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                         frac=round(achieved / PEAK_HBM_GBS, 4), traffic=None,
-                        kernel="decode_attn_kernel (cross-attention over the per-layer encoder K/V cache)",
+                        kernel="decode_attn_u2/u4_kernel (cross-attention over the per-layer encoder K/V cache)",
                         bytes_per_launch=int(ks["avg_work"]), avg_launch_ms=round(ks["avg_ms"], 5),
                         launches_timed=ks["launches"])
         out_d = {

@@ -30,13 +30,21 @@ namespace {
 
 using namespace twd;
 
-template <typename E>
-__global__ __launch_bounds__(DA_THREADS) void decode_attn_kernel(DecP p) {
+// U = loads in flight per lane, K/V streamed with nontemporal loads (round 4, tools/bench_decode_attn.py, same box,
+// profiles/r04_uv_decode_attn_ab.log): at the c4 shape (fp16, 512 clips x 20 heads over 1500 frames) U = 4 plain
+// 665 us, U = 4 nontemporal 620, U = 2 nontemporal 609 (6.45 TB/s), U = 8 782 (occupancy); at 128 x 20 pairs
+// U = 4 nontemporal 168 vs U = 2 190 -- hence U = 2 from DA_BIG pairs.
+template <typename E, int U>
+__device__ __forceinline__ void decode_attn_pair(const DecP& p) {
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
   int tk = p.Tk + (p.tk_dev ? *p.tk_dev : 0);
   if (tk > DA_MAX_TK) tk = DA_MAX_TK;
-  decode_attn_body<E>(p, b, h, 0, tk, nullptr);
+  decode_attn_body<E, U, true>(p, b, h, 0, tk, nullptr);
 }
+template <typename E>
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_u4_kernel(DecP p) { decode_attn_pair<E, 4>(p); }
+template <typename E>
+__global__ __launch_bounds__(DA_THREADS) void decode_attn_u2_kernel(DecP p) { decode_attn_pair<E, 2>(p); }
 
 // split over keys (few (clip, head) pairs: batch-1 long-form): blockIdx.y = chunk of S keys; chunks past
 // the effective Tk store an empty partial (m = -inf, l = 0); decode_attn_combine_kernel merges them.
@@ -731,7 +739,8 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
       return TW_OK;
     }
   }
-  TW_LAUNCH_DT(dtype, decode_attn_kernel, dim3(B * H), dim3(DA_THREADS), p);
+  if (B * H >= DA_BIG) TW_LAUNCH_DT(dtype, decode_attn_u2_kernel, dim3(B * H), dim3(DA_THREADS), p);
+  else TW_LAUNCH_DT(dtype, decode_attn_u4_kernel, dim3(B * H), dim3(DA_THREADS), p);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

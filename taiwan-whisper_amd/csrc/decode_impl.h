@@ -8,6 +8,7 @@ constexpr int DA_THREADS = 256;
 constexpr int DA_MAX_TK = 2048;
 constexpr int DA_SPLIT = 128;   // keys per workgroup of the split (flash-decoding) variant
 constexpr int DA_U = 4;           // key sub-steps per wave iteration (loads in flight per lane)
+constexpr int DA_BIG = 4096;      // (clip, head) pairs from which the one-workgroup-per-pair kernel takes DA_U = 2
 
 struct DecP {
   const void* q; int64_t sqb;
@@ -19,12 +20,37 @@ struct DecP {
   float c;        // scale * log2(e)
 };
 
+// K / V rows of the one-workgroup-per-pair kernel are read once per decode step: NT streams them past the caches
+// (nontemporal loads, 16-bit forms; the fp32 path reads plainly)
+template <bool NT>
+__device__ __forceinline__ void load8_kv(const bf16* p, float* o) {
+  if constexpr (NT) {
+    const bf16x8 v = __builtin_nontemporal_load((const bf16x8*)p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(v[j]);
+  } else {
+    load8(p, o);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void load8_kv(const f16* p, float* o) {
+  if constexpr (NT) {
+    const f16x8 v = __builtin_nontemporal_load((const f16x8*)p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)v[j];
+  } else {
+    load8(p, o);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void load8_kv(const float* p, float* o) { load8(p, o); }
+
 // lane = (key slot ks = lane >> 3, 8-element chunk ch = lane & 7); a wave covers 8 keys per step.
 // E = bf16 (autocast path) or float (fp32 path: exact expf, no rounding of the output).
 // The body attends keys [lo, hi).  part == nullptr: normalise and store O.  Otherwise (split over keys,
 // flash-decoding) store the chunk's unnormalised o[64], its max m (log2 domain) and sum l to part[0..65]
 // for decode_attn_combine_kernel.
-template <typename E>
+template <typename E, int DA_U = twd::DA_U, bool NT = false>
 __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, int lo, int hi, float* part) {
   __shared__ float sc[DA_MAX_TK];
   __shared__ float red[DA_THREADS / 64][64];
@@ -46,7 +72,7 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
 #pragma unroll
     for (int u = 0; u < DA_U; ++u) {
       const int key = k0 + 8 * u + ks;
-      if (key < hi) load8(kb + (int64_t)key * p.ldk, t[u]);
+      if (key < hi) load8_kv<NT>(kb + (int64_t)key * p.ldk, t[u]);
     }
 #pragma unroll
     for (int u = 0; u < DA_U; ++u) {
@@ -80,7 +106,7 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
 #pragma unroll
     for (int u = 0; u < DA_U; ++u) {
       const int key = k0 + 8 * u + ks;
-      if (key < hi) load8(vb + (int64_t)key * p.ldv, t[u]);
+      if (key < hi) load8_kv<NT>(vb + (int64_t)key * p.ldv, t[u]);
     }
 #pragma unroll
     for (int u = 0; u < DA_U; ++u) {

@@ -1,6 +1,6 @@
 """tw_decode_attn A/B on the decode shapes: cross-attention over 1500 encoder frames (large-v2: H = 20)
-at batch 1 / 16 / 64 / 128; TW_DECODE_SPLIT selects the variant per process (0 never split, 1 default
-heuristic, 2 always split).  Prints us per call and the K/V read rate."""
+at batch 1 / 16 / 64 / 128 (bf16), or the batches and dtype given (`fp16 512`: the c4 pseudo-labelling shape).
+Prints us per call and the K/V read rate."""
 import os
 import sys
 
@@ -12,10 +12,12 @@ from tw import ops
 
 def main():
     H, Tk, d = 20, 1500, 1280
-    for B in (1, 16, 64, 128):
-        kv = torch.randn(B * Tk, 2 * d, device="cuda").bfloat16()
-        q = torch.randn(B, d, device="cuda").bfloat16()
-        o = torch.empty(B, d, dtype=torch.bfloat16, device="cuda")
+    dt = torch.float16 if "fp16" in sys.argv[1:] else torch.bfloat16
+    batches = [int(a) for a in sys.argv[1:] if a.isdigit()] or [1, 16, 64, 128]
+    for B in batches:
+        kv = torch.randn(B * Tk, 2 * d, device="cuda").to(dt)
+        q = torch.randn(B, d, device="cuda").to(dt)
+        o = torch.empty(B, d, dtype=dt, device="cuda")
         run = lambda: ops.decode_attn(q, d, kv, 2 * d, Tk * 2 * d, kv[:, d:], 2 * d, Tk * 2 * d, o, d, B, H, Tk, 0.125)
         for _ in range(3):
             run()
@@ -27,7 +29,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 50 * 1e3
-        print(f"split={os.environ.get('TW_DECODE_SPLIT', '1')} B={B:4d}: {us:8.1f} us  {B * Tk * 2 * d * 2 / us / 1e3:7.1f} GB/s",
+        print(f"{str(dt)[6:]} B={B:4d}: {us:8.1f} us  {B * Tk * 2 * d * 2 / us / 1e3:7.1f} GB/s",
               flush=True)
 
 
