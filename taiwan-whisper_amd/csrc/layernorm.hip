@@ -170,6 +170,18 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
   }
 }
 
+// 4 consecutive elements of a fp32 / bf16 / fp16 row as fp32 (one 16-B or 8-B load; i a multiple of 4, the base 16-B
+// aligned)
+__device__ __forceinline__ f32x4 ld4_as_f32(const void* p, int dtype, int64_t i) {
+  if (dtype == TW_F32) return *(const f32x4*)((const float*)p + i);
+  if (dtype == TW_BF16) {
+    const bf16x4 t = *(const bf16x4*)((const bf16*)p + i);
+    return f32x4{bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3])};
+  }
+  const f16x4 t = *(const f16x4*)((const f16*)p + i);
+  return f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+}
+
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)); dx accumulated into dx_out (fp32).
 // Per-block partial dw/db written to partial[blockIdx.x][2][D] for a column reduction.
 template <int VEC, int MAXJ>
@@ -192,14 +204,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x,
     const float mu = mean_in[row], rs = rstd_in[row];
     float xh[MAXJ][VEC], g[MAXJ][VEC];
     float s1 = 0.f, s2 = 0.f;
+    // VEC 4: each lane's 4 consecutive x / dy values as one 16-B (fp32) or 8-B (16-bit) load, every load of the row
+    // issued before the arithmetic (the host checks the 16-B alignment); else one element per lane and load
+    float xs[MAXJ][VEC], ds[MAXJ][VEC];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (j < J) {
+        if constexpr (VEC == 4) {
+          const int64_t e = base + (j * 64 + lane) * 4;
+          const f32x4 a = ld4_as_f32(x, x_dtype, e), c = ld4_as_f32(dy, dy_dtype, e);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { xs[j][q] = a[q]; ds[j][q] = c[q]; }
+        } else {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            const int e = (j * 64 + lane) * VEC + q;
+            xs[j][q] = ld_as_f32(x, x_dtype, base + e);
+            ds[j][q] = ld_as_f32(dy, dy_dtype, base + e);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
       if (j < J) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q) {
           const int e = (j * 64 + lane) * VEC + q;
-          const float xv = ld_as_f32(x, x_dtype, base + e);
-          const float dv = ld_as_f32(dy, dy_dtype, base + e);
+          const float xv = xs[j][q];
+          const float dv = ds[j][q];
           xh[j][q] = (xv - mu) * rs;
           g[j][q] = dv * w[e];
           s1 += g[j][q];
@@ -214,11 +247,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x,
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
       if (j < J) {
+        if constexpr (VEC == 4) {
+          float* d = dx + base + (j * 64 + lane) * 4;
+          f32x4 o;
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) {
-          const int e = (j * 64 + lane) * VEC + q;
-          const float o = rs * (g[j][q] - s1 - xh[j][q] * s2);
-          if (dx_accum) dx[base + e] += o; else dx[base + e] = o;
+          for (int q = 0; q < 4; ++q) o[q] = rs * (g[j][q] - s1 - xh[j][q] * s2);
+          if (dx_accum) o += *(const f32x4*)d;
+          *(f32x4*)d = o;
+        } else {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            const int e = (j * 64 + lane) * VEC + q;
+            const float o = rs * (g[j][q] - s1 - xh[j][q] * s2);
+            if (dx_accum) dx[base + e] += o; else dx[base + e] = o;
+          }
         }
       }
     }
@@ -359,7 +401,7 @@ extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, cons
   int nblk = (rows + WPB - 1) / WPB;
   if (nblk > 1024) nblk = 1024;
   if (workspace_floats < (int64_t)nblk * 2 * D) return TW_EINVAL;
-  if (D % 256 == 0)
+  if (D % 256 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w) & 15) == 0)
     hipLaunchKernelGGL((ln_bwd_kernel<4, 5>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy, dy_dtype,
                        dx, dx_accum, workspace, rows, D);
   else

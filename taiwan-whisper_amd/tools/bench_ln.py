@@ -44,7 +44,40 @@ def run(rows, D, dt, add, reps=50):
           f"err={err:.3g} xerr={xerr:.3g}", flush=True)
 
 
+def run_bwd(rows, D, xdt, reps=30):
+    """tw_layernorm_bwd with dx accumulated (the student's fp32 stream): algorithmic bytes = read x, dy, dx and
+    write dx (the per-block dw / db partials and their reduction counted apart)."""
+    dev = "cuda"
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn(rows, D, generator=g).to(dev, xdt)
+    dy = torch.randn(rows, D, generator=g).to(dev)
+    w = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    mean = x.float().mean(1)
+    rstd = (x.float().var(1, unbiased=False) + 1e-5).rsqrt()
+    dx = torch.zeros(rows, D, device=dev)
+    dw = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    call = lambda: ops.layernorm_bwd(x, w, mean, rstd, dy, dx, dw, db, dx_accum=True)
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    nbytes = rows * D * (x.element_size() + 4 + 8)
+    print(f"bwd rows={rows:6d} D={D} {str(xdt):15s} {us:8.1f} us {nbytes / us / 1e3:7.1f} GB/s", flush=True)
+
+
 if __name__ == "__main__":
+    if "bwd" in sys.argv[1:]:
+        for rows, D in ((48000, 768), (96000, 1280), (14304, 768)):
+            for xdt in (torch.float32, torch.bfloat16):
+                run_bwd(rows, D, xdt)
+        sys.exit(0)
     for dt in (torch.bfloat16, torch.float16):
         for rows in (448 * 64, 1500 * 64, 512):
             for add in ((False, True) if dt == torch.bfloat16 else (False,)):

@@ -497,7 +497,7 @@ def test_gemm_batched_strided_view():
 
 
 # ----------------------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("D", [64, 384, 512, 1280])
+@pytest.mark.parametrize("D", [64, 384, 512, 768, 1280])
 @pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
 def test_layernorm(D, xdt):
     from tw import ops
