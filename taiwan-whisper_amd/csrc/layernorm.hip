@@ -401,9 +401,21 @@ extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, cons
   int nblk = (rows + WPB - 1) / WPB;
   if (nblk > 1024) nblk = 1024;
   if (workspace_floats < (int64_t)nblk * 2 * D) return TW_EINVAL;
-  if (D % 256 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w) & 15) == 0)
-    hipLaunchKernelGGL((ln_bwd_kernel<4, 5>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy, dy_dtype,
-                       dx, dx_accum, workspace, rows, D);
+  // VEC 4 with the exact number of 256-column chunks as MAXJ: the per-lane arrays (x, dy, xhat, g, dw, db) sized
+  // for the row, not for D = 1280 (D = 768: fewer registers, more waves per SIMD)
+  const bool v4 = D % 256 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w) & 15) == 0;
+#define TW_LN_BWD(J)                                                                                          \
+  hipLaunchKernelGGL((ln_bwd_kernel<4, J>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy, dy_dtype, \
+                     dx, dx_accum, workspace, rows, D)
+  // D = 1280 holds 162 VGPRs = 3 waves per SIMD: 768 blocks (all resident at once) instead of a 1024-block grid
+  // whose last quarter would run as a second, mostly idle round
+  if (v4 && D > 1024 && nblk > 768) nblk = 768;
+  if (v4 && D == 256) TW_LN_BWD(1);
+  else if (v4 && D == 512) TW_LN_BWD(2);
+  else if (v4 && D == 768) TW_LN_BWD(3);
+  else if (v4 && D == 1024) TW_LN_BWD(4);
+  else if (v4) TW_LN_BWD(5);
+#undef TW_LN_BWD
   else
     hipLaunchKernelGGL((ln_bwd_kernel<1, 20>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy,
                        dy_dtype, dx, dx_accum, workspace, rows, D);
