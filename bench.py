@@ -100,7 +100,10 @@ def cpu_baseline(seconds_budget=20.0):
     from oracle import distill_ref, labels as L, logmel
     from oracle.weights import CONFIGS, make_weights
     from oracle.whisper_ref import Ref, to_torch
-    threads = min(16, os.cpu_count() or 1)
+    # the job's CPU share: OMP_NUM_THREADS where the launcher sets it (the GPU box gives a 1-GPU job 16 threads of a
+    # much larger host), else every CPU this process may run on
+    host = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0)) or host
     torch.set_num_threads(threads)
     cfg = CONFIGS["tiny"]
     ps = to_torch(make_weights(cfg, 1))
@@ -129,7 +132,9 @@ def cpu_baseline(seconds_budget=20.0):
             break
     steady = times[1:] if len(times) > 1 else times
     per = sum(steady) / len(steady)
-    return dict(value=round(B / per, 4), unit="utt/s", cores=threads, kind="port",
+    return dict(value=round(B / per, 4), unit="utt/s", cores=threads, host_cores=host,
+                cores_note=f"{threads} threads = this job's CPU share (OMP_NUM_THREADS / affinity) of a host with "
+                           f"{host} logical CPUs", kind="port",
                 sample=f"config 1 (tiny<-tiny, B=2, fp32, frozen shared encoder, CPU log-mel + train_step + "
                        f"AdamW) via oracle/distill_ref.py, {len(steady)} steady steps of {len(times)}")
 
@@ -317,6 +322,42 @@ def run_decode(args, device, rank, world, pg):
         torch.distributed.destroy_process_group()
 
 
+def exchange_summary(ev, log, steps, t_rank, pg, world, device):
+    """The `distributed` object of the JSON line (collective over the ranks: every rank calls it).
+    ev: the trainer's exchange_events, (start, layers done, tail done) events per timed exchange wait on the compute
+    stream (anything with .elapsed_time); log: its exchange_log, (bytes, tail) per all-reduced bucket; t_rank: this
+    rank's own time for the timed steps, taken before the closing barrier."""
+    if pg is None:
+        return dict(backend=None, world_size=1, exchange=None)
+    # compute-stream time between reaching the gradient-exchange wait and passing it (the all-reduce time the step
+    # does not hide), per timed step: the buckets launched per finished layer during the backward, then the tail
+    # launched after it (tied embedding + final LayerNorm, final only after the embedding backward)
+    layers_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+    tail_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+    backend = torch.distributed.get_backend(pg)
+    per_rank = torch.tensor([t_rank / steps * 1e3, layers_ms + tail_ms], dtype=torch.float64,
+                            device="cpu" if backend == "gloo" else device)
+    gathered = [torch.zeros_like(per_rank) for _ in range(world)]
+    torch.distributed.all_gather(gathered, per_rank, group=pg)
+    step_ms = [float(g[0]) for g in gathered]
+    exposed = [float(g[1]) for g in gathered]
+    nbytes = sum(b for b, _ in log) / steps
+    tail_bytes = sum(b for b, t in log if t) / steps
+    return dict(backend=backend, world_size=torch.distributed.get_world_size(pg),
+                exchange_bytes_per_step=int(nbytes), exchange_tail_bytes_per_step=int(tail_bytes),
+                exchange_buckets_per_step=len(log) // steps,
+                # a ring all-reduce moves 2 (N - 1) / N of the payload in and out of every GPU
+                ring_bytes_per_gpu_per_step=int(2 * (world - 1) / world * nbytes),
+                exchange_exposed_ms_per_step=round(layers_ms + tail_ms, 3),
+                exchange_exposed_layers_ms_per_step=round(layers_ms, 3),
+                exchange_exposed_tail_ms_per_step=round(tail_ms, 3),
+                rank_step_ms=[round(x, 3) for x in step_ms],
+                rank_step_ms_spread=round(max(step_ms) - min(step_ms), 3),
+                rank_exchange_exposed_ms=[round(x, 3) for x in exposed],
+                exchange="bucketed async SUM all-reduce of the flat fp32 student gradient, launched per finished "
+                         "layer during the backward; clip + AdamW deferred under the next encoder forward")
+
+
 def load_mfma(workload, family):
     """MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)) of a kernel family
     from the committed rocprofv3 --pmc summary (tools/pmc_mfma.sh -> profiles/mfma_latest.json)."""
@@ -409,6 +450,7 @@ def main():
     trainer = DistillationTrainer(student, teacher, learning_rate=1e-4, warmup_steps=0,
                                   freeze_encoder=freeze_encoder, process_group=pg)
     trainer.exchange_events = [] if pg is not None else None     # exposed gradient-exchange waits
+    trainer.exchange_log = [] if pg is not None else None        # (bytes, tail) per all-reduced bucket
     fe = WhisperFeatureExtractor(device=device)
     batches = make_batches(args, device, rank)
 
@@ -423,6 +465,7 @@ def main():
     torch.cuda.synchronize()
     if trainer.exchange_events is not None:
         trainer.exchange_events.clear()
+        trainer.exchange_log.clear()
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -433,6 +476,7 @@ def main():
             m = step(i)
         trainer.flush()          # ... and the last timed step's update inside it: exactly K updates timed
         torch.cuda.synchronize()
+        t_rank = time.perf_counter() - t0            # this rank's own time, before the closing barrier
         if pg is not None:
             torch.distributed.barrier()
         torch.cuda.synchronize()
@@ -443,17 +487,7 @@ def main():
     elapsed = float(elapsed.item())
     loss = float(m["loss"].item())
     ks = timer.summary()
-    exch_ms = None
-    if trainer.exchange_events is not None:
-        # compute-stream time between reaching the gradient-exchange wait and passing it (the all-reduce time
-        # the step does not hide), per timed step
-        exch_ms = sum(a.elapsed_time(b) for a, b in trainer.exchange_events) / args.steps
-    dist = dict(backend=torch.distributed.get_backend(pg) if pg is not None else None,
-                world_size=torch.distributed.get_world_size(pg) if pg is not None else 1,
-                exchange_exposed_ms_per_step=None if exch_ms is None else round(exch_ms, 3),
-                exchange="bucketed async SUM all-reduce of the flat fp32 student gradient, launched per finished "
-                         "layer during the backward; clip + AdamW deferred under the next encoder forward"
-                if pg is not None else None)
+    dist = exchange_summary(trainer.exchange_events, trainer.exchange_log, args.steps, t_rank, pg, world, device)
 
     teacher_ms = None
     if not args.no_teacher_fwd:

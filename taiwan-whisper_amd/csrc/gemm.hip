@@ -1033,7 +1033,7 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (!a_trans && !b_trans && !(flags & (16384 | 256 | 512 | 1024 | 2048 | 262144))) {
     int m_dp = 0;
     // (fp16: the persistent part must be whole 256x256 tiles with a fast epilogue)
-    if (dp_tail_plan(p, batch, m_dp) && (!H || ((N % 256) == 0 && p.epi != EPI_GENERIC)) &&
+    if (dp_tail_plan(p, batch, m_dp) && (!H || ((N % 256) == 0 && (K % BK) == 0 && p.epi != EPI_GENERIC)) &&
         launch_dp_tail<H>(p, m_dp, stream))
       return TW_OK;
   }

@@ -4,6 +4,8 @@
 // output bf16 (feeds the next bf16 GEMM) or fp32.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int WPB = 4;   // waves (rows) per block
@@ -407,9 +409,19 @@ extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, cons
 #define TW_LN_BWD(J)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_kernel<4, J>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy, dy_dtype, \
                      dx, dx_accum, workspace, rows, D)
-  // D = 1280 holds 162 VGPRs = 3 waves per SIMD: 768 blocks (all resident at once) instead of a 1024-block grid
-  // whose last quarter would run as a second, mostly idle round
-  if (v4 && D > 1024 && nblk > 768) nblk = 768;
+  // D = 1280 holds 162 VGPRs = 3 waves per SIMD: one block per resident slot (768 on a 256-CU MI355X: all resident
+  // at once) instead of a 1024-block grid whose last quarter would run as a second, mostly idle round.  The cap is
+  // the occupancy query x the device's CU count (cached), not a constant of one part.
+  if (v4 && D > 1024) {
+    static const int cap = [] {
+      int dev = 0, cus = 0, per = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ln_bwd_kernel<4, 5>, 256, 0);
+      return std::max(1, cus) * std::max(1, per);
+    }();
+    if (nblk > cap) nblk = cap;
+  }
   if (v4 && D == 256) TW_LN_BWD(1);
   else if (v4 && D == 512) TW_LN_BWD(2);
   else if (v4 && D == 768) TW_LN_BWD(3);

@@ -107,7 +107,10 @@ class DistillationTrainer:
         if self.overlap_update and not freeze_encoder:
             raise ValueError("overlap_update needs a frozen encoder: the next forward must read no trainable weight")
         self._update = None      # (lr, t) of a launched, not yet applied update
-        self.exchange_events = None   # list -> (start, end) events around each exchange wait (bench.py)
+        # bench.py instrumentation: with lists here, wait_grad_exchange() appends (start, layers done, tail done)
+        # events around each exchange wait and _launch() appends (bytes, tail) per all-reduced slice
+        self.exchange_events = None
+        self.exchange_log = None
         set_trainable_like_reference(student, freeze_encoder, freeze_decoder, freeze_embed_positions)
         self.train_encoder = not freeze_encoder
         self.freeze_encoder, self.freeze_decoder = freeze_encoder, freeze_decoder
@@ -224,13 +227,17 @@ class DistillationTrainer:
         return {"loss": out3[0], "ce_loss": out3[1], "kl_loss": out3[2]}
 
     # ------------------------------------------------------------------ update
-    def _launch(self, lo, hi):
+    def _launch(self, lo, hi, tail=False):
+        """Async SUM all-reduce of grad[lo:hi) in buckets.  tail: launched after the backward (the ranges no
+        layer hook covered: the embeddings, the final LayerNorm), i.e. the part that cannot overlap it."""
         g = self.s.grad
         for a in range(lo, hi, self.bucket):
             sl = g[a: min(hi, a + self.bucket)]
             if not self.fold_world:
                 sl.mul_(1.0 / self.world)          # DDP: grad * fp32(1/world) into the bucket, then SUM
-            self._pending.append(torch.distributed.all_reduce(sl, group=self.pg, async_op=True))
+            self._pending.append((torch.distributed.all_reduce(sl, group=self.pg, async_op=True), tail))
+            if getattr(self, "exchange_log", None) is not None:
+                self.exchange_log.append((sl.numel() * sl.element_size(), tail))
         self._reduced.append((lo, hi))
 
     def _grad_ready(self, prefix):
@@ -251,25 +258,32 @@ class DistillationTrainer:
             self._pending = []
         for lo, hi in done + [(self.s.grad.numel(), self.s.grad.numel())]:
             if lo > pos:
-                self._launch(pos, lo)
+                self._launch(pos, lo, tail=True)
             pos = max(pos, hi)
         self._reduced = []
         self.bw.on_ready = None
 
     def wait_grad_exchange(self):
         """The compute stream waits for every launched bucket (a stream dependency under RCCL).  With
-        `exchange_events` a list (bench.py), an event pair brackets the wait on the compute stream: their
-        distance is the exchange time the step leaves exposed."""
+        `exchange_events` a list (bench.py), events bracket the wait on the compute stream: first the buckets
+        launched during the backward (per finished layer), then the tail launched after it (the tied embedding,
+        final LayerNorm).  Their distances are the exchange time the step leaves exposed, split into the two."""
         pend = getattr(self, "_pending", [])
         ev = getattr(self, "exchange_events", None) if pend else None
         if ev is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        for w in pend:
-            w.wait()
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+        for w, tail in pend:            # RCCL runs them in launch order: layers first, then the tail
+            if not tail:
+                w.wait()
         if ev is not None:
-            e1.record()
-            ev.append((e0, e1))
+            e[1].record()
+        for w, tail in pend:
+            if tail:
+                w.wait()
+        if ev is not None:
+            e[2].record()
+            ev.append(tuple(e))
         self._pending, self._reduced = [], []
 
     def all_reduce_grads(self):

@@ -117,6 +117,8 @@ def _linear_gelu_setup(ctx, inputs, output):
 
 def _linear_gelu_bwd(ctx, g, _gpre):
     x, w, pre = ctx.saved_tensors
+    if g.dtype != torch.bfloat16 or pre.dtype != torch.bfloat16:
+        raise NotImplementedError("tw ops: backward is a bf16 (autocast) path; the fp16 model is forward-only")
     dpre = torch.empty_like(pre)
     F.gelu_bwd(g.contiguous(), pre, dpre)             # round16(g * gelu'(pre)): the DGELU epilogue's arithmetic
     dx, dw, db = _lin_bwd(dpre, x, w, ctx.has_b)

@@ -211,3 +211,76 @@ def test_deferred_update_control_flow():
     out = mp.Manager().dict()
     mp.spawn(_worker_deferred, args=(2, _free_port(), out), nprocs=2, join=True)
     assert out[0] and out[1]
+
+
+def _worker_world4(rank, world, port, out):
+    """World 4: the per-layer exchange is launched in backward order as each layer's
+    gradients become final (last decoder layer first), the tail (embeddings + final LayerNorm, no layer hook)
+    after the backward, each slice cut into buckets in address order; exchange_log records bytes and the
+    tail flag per bucket; with overlap_update nothing is applied until flush(), which then sees the DDP mean."""
+    import sys
+    import types
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "taiwan-whisper_amd"))
+    import tw.distill as D
+    _init(rank, world, port)
+    launched = []
+    real_ar = dist.all_reduce
+
+    def rec_ar(t, group=None, async_op=False):
+        launched.append((t.data_ptr() - base[0]) // 4)
+        return real_ar(t, group=group, async_op=async_op)
+    D.torch.distributed.all_reduce = rec_ar
+    calls = []
+    D.F = types.SimpleNamespace(l2norm=lambda g, norm, ws: (calls.append(("norm", g.clone())), norm.fill_(float(g.norm()))),
+                                adamw=lambda p32, g, m, v, p16, lr, b1, b2, eps, wd, t, norm, mx:
+                                calls.append(("adamw", lr, t)))
+
+    class Stub:
+        pass
+    # flat gradient layout of a 2-decoder-layer student: [layer0 | layer1 | embed_tokens + final LN] (sizes uneven)
+    ranges = {"model.decoder.layers.0.": (0, 3000), "model.decoder.layers.1.": (3000, 7000)}
+    n = 12_345
+    st = D.DistillationTrainer.__new__(D.DistillationTrainer)
+    st.s, st.bw = Stub(), Stub()
+    g0 = torch.randn(n, generator=torch.Generator().manual_seed(rank))
+    st.s.grad = g0 / world                        # power-of-two world: 1/world folded into the loss gradient
+    base = [st.s.grad.data_ptr()]
+    st.s.grad_range = lambda prefix: ranges.get(prefix)
+    st.s.store = Stub()
+    st.s.store.p32 = st.s.store.p16 = torch.zeros(n)
+    st.m_buf, st.v_buf = torch.zeros(n), torch.zeros(n)
+    st.world, st.pg, st.bucket, st.fold_world = world, dist.group.WORLD, 2048, True
+    st.norm, st.ws = torch.zeros(1), torch.zeros(8)
+    st.runs = [(0, n, 0.0)]
+    st.lr, st.warmup, st.sched, st.step = 1e-3, 0, "constant", 0
+    st.b1 = st.b2 = st.eps = st.wd = 0.0
+    st.max_grad_norm = 1.0
+    st.overlap_update, st._update = True, None
+    st.exchange_log, st.exchange_events = [], None
+    st._pending, st._reduced = [], []
+    st.bw.on_ready = st._grad_ready
+    # the backward finishes the layers last-first and fires the hook per layer
+    st.bw.on_ready("model.decoder.layers.1.")
+    st.bw.on_ready("model.decoder.layers.0.")
+    st.optimizer_step()                           # launches the tail, defers the update
+    assert calls == [] and st._update == (1e-3, 1) and st.bw.on_ready is None
+    assert launched == [3000, 5048, 0, 2048, 7000, 9048, 11096], launched
+    assert [b for b, _ in st.exchange_log] == [4 * x for x in (2048, 1952, 2048, 952, 2048, 2048, 1249)]
+    assert [t for _, t in st.exchange_log] == [False] * 4 + [True] * 3
+    assert sum(b for b, _ in st.exchange_log) == 4 * n
+    st.flush()
+    assert [c[0] for c in calls] == ["norm", "adamw"] and calls[1][1:] == (1e-3, 1)
+    out[rank] = calls[0][1]
+    dist.destroy_process_group()
+
+
+def test_world4_launch_order_and_deferred_update():
+    world = 4
+    out = mp.Manager().dict()
+    mp.spawn(_worker_world4, args=(world, _free_port(), out), nprocs=world, join=True)
+    n = 12_345
+    g = [torch.randn(n, generator=torch.Generator().manual_seed(r)) for r in range(world)]
+    mean = sum(x / world for x in g)
+    for r in range(world):
+        assert torch.equal(out[r], out[0])
+        assert torch.allclose(out[r], mean, rtol=1e-6, atol=1e-7)

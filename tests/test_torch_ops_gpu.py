@@ -5,9 +5,8 @@
   from the torch operators is BIT-IDENTICAL to the engine's own ctypes path (WhisperForConditionalGeneration.decode)
   on the micro config, bf16 model: the operators run the same kernels with the same arguments.
 * Autograd through the operators (register_autograd -> the HIP backward kernels) against an fp32 torch autograd
-  reference of the same layer: cosine >= 0.999 and relative L2 <= 3e-2 per gradient, 6e-2 for the LayerNorm
-  weights (sums over rows of bf16-rounded products; bf16 operands and rounding points, as the reference's
-  autocast backward).
+  reference of the same layer: cosine >= 0.999 and relative L2 <= max(3e-2, 2 x the distance of the same layer
+  under torch bf16 autocast -- the reference's own arithmetic -- to fp32) per gradient.
 * torch.library.opcheck: schema, autograd registration and fake-tensor consistency of every trainable op.
 """
 import pytest
@@ -159,12 +158,21 @@ def test_layer_autograd_vs_fp32_torch():
     assert _rel(out16, out32) < 1e-2
     (out16 * G).sum().backward()
     (out32 * G).sum().backward()
+    # the reference's own arithmetic: the same fp32 layer under torch bf16 autocast (run_distillation.py runs the
+    # student under Accelerator(mixed_precision="bf16")); its distance to fp32 is the noise floor a bf16 backward has
+    PA = {k: v.detach().float().clone().requires_grad_(True) for k, v in W.items()}
+    xa = x0.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        outa = run_ref(PA, xa)
+    (outa.float() * G).sum().backward()
     torch.cuda.synchronize()
-    pairs = [("x", x16.grad, x32.grad)] + [(k, P16[k].grad, P32[k].grad) for k in P16]
-    for k, a, b in pairs:
+    pairs = [("x", x16.grad, x32.grad, xa.grad)] + [(k, P16[k].grad, P32[k].grad, PA[k].grad) for k in P16]
+    for k, a, b, c in pairs:
         assert a is not None, k
-        bound = 6e-2 if k.startswith("ln") else 3e-2
-        assert _rel(a, b) <= bound and _cos(a, b) >= 0.999, (k, _rel(a, b), _cos(a, b))
+        # 3e-2, or twice the autocast reference's own distance to fp32 where that is larger (the LayerNorm weights:
+        # sums over rows of bf16-rounded products; the round-4 bound of 6e-2 for them is replaced by this measure)
+        bound = max(3e-2, 2 * _rel(c, b))
+        assert _rel(a, b) <= bound and _cos(a, b) >= 0.999, (k, _rel(a, b), _cos(a, b), "autocast ref", _rel(c, b))
 
 
 def test_kl_ce_op_gradient_is_the_fused_kernel():
@@ -195,6 +203,17 @@ def test_log_mel_op_matches_feature_extractor():
     ref, _ = WhisperFeatureExtractor(device=torch.device(DEV)).extract(wav, want_conv_input=False)
     torch.cuda.synchronize()
     assert torch.equal(mel, ref)
+
+
+def test_fp16_backward_raises_not_implemented():
+    """The fp16 model is forward-only: every trainable op's backward raises NotImplementedError."""
+    g = torch.Generator(device=DEV).manual_seed(2)
+    x = (torch.randn(64, 128, device=DEV, generator=g) * 0.3).half().requires_grad_(True)
+    w = (torch.randn(256, 128, device=DEV, generator=g) * 0.3).half().requires_grad_(True)
+    for op in (lambda: torch.ops.tw.linear_gelu(x, w, None)[0], lambda: torch.ops.tw.linear(x, w, None)):
+        y = op()
+        with pytest.raises(NotImplementedError):
+            y.float().sum().backward()
 
 
 @pytest.mark.parametrize("op", ["linear", "linear_gelu", "linear_residual", "layer_norm", "attention"])
