@@ -639,6 +639,40 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
             cand = cand[:k] if pad == eos else cand[:k - 1]
         return cand
 
+    def seeds_of(b, nwin):
+        return [(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1) for fi in range(len(temps))]
+
+    # First windows as batches: every clip's first window has the same prompt, so the first attempt of
+    # up to 8 clips' first windows is encoded and decoded as ONE batch, as HF's seek loop keeps its batch together
+    # (a short-form timestamp call is then one batched decode, not B batch-1 decodes).  Rows are independent on the
+    # 16-bit paths (batch_rows_independent), so each row's tokens and gates are those of its clip's own attempt 0;
+    # the per-clip loop below takes them over and continues (fallback attempts, later windows) clip by clip.
+    first = {}
+    live = [b for b in range(B) if int(lens[b]) > 0]
+    if len(live) > 1 and batch_rows_independent(model):
+        P0 = len(init)
+        ml0 = total_length(cfg, gc, P0, max_length, max_new_tokens)
+        ns0 = (0, ns_token) if no_speech_threshold is not None else None
+        for c0 in range(0, len(live), 8):
+            rows = live[c0:c0 + 8]
+            nb = len(rows)
+            segb = torch.zeros(nb, nmel, window, dtype=torch.float32, device=dev)
+            for i, b in enumerate(rows):
+                n = min(window, int(lens[b]))
+                segb[i, :, :n] = feats[b, :, :n]
+            enc_all = model.encode(model.conv_input(segb))
+            Tk_ = enc_all.shape[0] // nb
+            d_ = decoder(P0, ml0, nb)
+            tl = [temps[0] or 0.0] * nb
+            sl = [seeds_of(b, 0)[0] for b in rows]
+            raws = d_.run(enc_all, torch.tensor([init] * nb, dtype=torch.int64, device=dev),
+                          temperature=tl if nb > 1 else tl[0], seed=sl if nb > 1 else sl[0], no_speech=ns0).tolist()
+            for i, b in enumerate(rows):
+                raw = row_tokens(raws[i], eos)
+                avg = float(d_.sel.sum_logp[i]) / max(len(trim(raw)), 1) if track else 0.0
+                nsp = float(torch.exp(d_.ns_logp[i])) if ns0 is not None else 0.0
+                first[b] = (raw, avg, nsp, enc_all[i * Tk_:(i + 1) * Tk_], nb)
+
     seg_in = torch.zeros(1, nmel, window, dtype=torch.float32, device=dev)
     outs = []
     for b in range(B):
@@ -647,9 +681,13 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
         cond = bool(condition_on_prev_tokens)
         while seek < Tb:
             n = min(window, Tb - seek)
-            seg_in.zero_()
-            seg_in[0, :, :n] = feats[b, :, seek:seek + n]
-            enc16 = model.encode(model.conv_input(seg_in))
+            pre = first.pop(b, None) if nwin == 0 else None
+            if pre is not None:
+                enc16 = pre[3]
+            else:
+                seg_in.zero_()
+                seg_in[0, :, :n] = feats[b, :, seek:seek + n]
+                enc16 = model.encode(model.conv_input(seg_in))
             prompt = list(init)
             if cond and segments and prev_sot is not None:
                 prev = []
@@ -669,7 +707,7 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
             # batch costs about what one attempt does.  Rows are independent (per-row temperature / seed,
             # tw_select_sample_ts), so each row decodes exactly the tokens its sequential attempt would, and the
             # first passing row in temperature order is accepted, as HF generate_with_fallback accepts it.
-            seeds = [(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1) for fi in range(len(temps))]
+            seeds = seeds_of(b, nwin)
             attempts = [(0, dec, enc16, ptens, [temps[0] or 0.0], [seeds[0]])]
             rest = list(range(1, len(temps)))
             # fallback_batch=False: one attempt at a time (A/B, tests); so does the fp32 compute path, whose rows are
@@ -679,16 +717,20 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                 grp = rest[fb:fb + per]
                 attempts.append((grp[0], None, None, None, [temps[f] or 0.0 for f in grp], [seeds[f] for f in grp]))
             for fi0, d_, e_, p_, tl, sl in attempts:
-                if d_ is None:                               # a speculative batch of the remaining attempts
-                    nb = len(tl)
-                    d_ = decoder(P, ml, nb)
-                    e_ = enc16                               # shared by the rows (DecodeSession.set_encoder)
-                    p_ = ptens.repeat(nb, 1)
-                raws = d_.run(e_, p_, temperature=tl if len(tl) > 1 else tl[0], seed=sl if len(sl) > 1 else sl[0],
-                              no_speech=ns).tolist()
-                # a batch is cut at its LAST row's first eos, so a row that finished earlier carries extra eos (=pad)
-                # columns; each row is cut at its own first eos, which is exactly what its batch-1 decode returns
-                raws = [row_tokens(r, eos) for r in raws]
+                if fi0 == 0 and pre is not None:             # attempt 0 ran in the first-window batch
+                    raws, gates, nbatch = [pre[0]], [(pre[1], pre[2])], pre[4]
+                else:
+                    if d_ is None:                           # a speculative batch of the remaining attempts
+                        nb = len(tl)
+                        d_ = decoder(P, ml, nb)
+                        e_ = enc16                           # shared by the rows (DecodeSession.set_encoder)
+                        p_ = ptens.repeat(nb, 1)
+                    raws = d_.run(e_, p_, temperature=tl if len(tl) > 1 else tl[0],
+                                  seed=sl if len(sl) > 1 else sl[0], no_speech=ns).tolist()
+                    # a batch is cut at its LAST row's first eos, so a row that finished earlier carries extra eos
+                    # (=pad) columns; each row is cut at its own first eos, which is what its batch-1 decode returns
+                    raws = [row_tokens(r, eos) for r in raws]
+                    gates, nbatch = None, len(raws)
                 done_here = False
                 for r, raw in enumerate(raws):
                     fi, temp = fi0 + r, temps[fi0 + r]
@@ -696,16 +738,20 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                     needs = False
                     if track or compression_ratio_threshold is not None:
                         tg = time.perf_counter()      # gate cost: log-prob / no-speech readback + compression ratio
-                        avg = float(d_.sel.sum_logp[r]) / max(len(cand), 1) if track else 0.0
-                        nsp = float(torch.exp(d_.ns_logp[r])) if ns is not None else 0.0
+                        if gates is not None:
+                            avg, nsp = gates[r]
+                        else:
+                            avg = float(d_.sel.sum_logp[r]) / max(len(cand), 1) if track else 0.0
+                            nsp = float(torch.exp(d_.ns_logp[r])) if ns is not None else 0.0
                         needs, skip = need_fallback(cand, avg, nsp, V, compression_ratio_threshold, logprob_threshold,
                                                     no_speech_threshold)
                         if trace is not None:
                             trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw),
                                               avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip,
-                                              batch=len(raws), gate_ms=(time.perf_counter() - tg) * 1e3))
+                                              batch=nbatch, gate_ms=(time.perf_counter() - tg) * 1e3))
                     elif trace is not None:
-                        trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw)))
+                        trace.append(dict(b=b, seek=seek, n=n, T=temp, prompt=list(prompt), raw=list(raw),
+                                          batch=nbatch))
                     seq, t_acc = raw, temp
                     if not needs:
                         done_here = True
