@@ -427,56 +427,85 @@ LV2_SEED = 61
 
 
 def lv2_features():
-    """Two 30 s synthetic clips (the bench's sine + noise recipe) and a 45 s long-form input (the first 4 500 frames
-    of longform_features' deterministic draw)."""
-    short = logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(3, 14.0)])
+    """Four 30 s synthetic clips (the bench's sine + noise recipe, different seeds and tone lengths) and a 45 s
+    long-form input (the first 4 500 frames of longform_features' deterministic draw)."""
+    short = logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(3, 14.0),
+                                  logmel.synthetic_clip(5, 22.0), logmel.synthetic_clip(8, 30.0)])
     return short, longform_features()[:, :, :4500]
+
+
+def lv2_greedy_config():
+    from transformers import GenerationConfig
+    return GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
+                            pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
+                            begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=448, num_beams=1, do_sample=False,
+                            no_timestamps_token_id=SPECIAL["notimestamps"])
 
 
 def gen_lv2_decode(out):
     """HF generate at the REAL large-v2 dimensions (d 1280, 32 + 32 layers, 20 heads) -- the model of BASELINE c4 / c5
-    -- with documented random weights (oracle/weights.make_weights(large-v2, LV2_SEED, per_tensor=True,
-    embed_std=0.05)), in fp32 and with torch_dtype=float16 (run_eval.py:99, run_pseudo_labelling.py:461-463):
-      {f32,f16}_greedy_ids / _margin : greedy, 2 clips, [SOT, zh, transcribe, notimestamps], 48 new tokens
-                                       (run_pseudo_labelling.py:917-922 without timestamps)
-      {f32,f16}_ts_ids / _margin     : return_timestamps=True, language zh, 48 new tokens
-      f32_long_ids, f32_long_avg_logprobs, f32_long_ns_probs : 45 s long-form (2 windows), temperature (0.0,),
-                                       thresholds that never fire, per-window gates (run_eval.py:659-665 path)
+    -- with the documented decode-parity weights (oracle/weights.lv2_decode_weights(large-v2, LV2_SEED): the decoder's
+    cross-attention and positions strengthened so that decoding depends on the audio, round 5), in three arithmetics:
+      f32  fp32 model (mixed_precision "no")
+      f16  torch_dtype=float16 model, no autocast (run_eval.py:99, run_pseudo_labelling.py:461-463)
+      b16  fp32 model under torch.autocast("cpu", bfloat16) (run_distillation.py:1580-1584: generate_step runs the
+           student under the bf16 Accelerator)
+    and these calls:
+      {tag}_greedy_ids / _margin : greedy, 4 clips, [SOT, zh, transcribe, notimestamps], 48 new tokens
+                                   (run_pseudo_labelling.py:917-922 without timestamps)
+      {tag}_ts_ids / _margin     : return_timestamps=True, language zh, 48 new tokens, one clip per call (rows
+                                   padded with -1; margins [step, clip], nan-padded)
+      f32_long_ids, _long_avg_logprobs, _long_ns_probs, _long_margin, _long_window_steps : 45 s long-form (2 windows),
+                                   temperature (0.0,), thresholds that never fire, per-window gates (run_eval.py:659-665)
     _margin = per step and row, the top-1 minus top-2 processed score (_MarginSpy)."""
-    from transformers import GenerationConfig
+    import contextlib
     from transformers.generation.logits_process import LogitsProcessorList
+    from oracle.weights import lv2_decode_weights
     cfg = CONFIGS["large-v2"]
-    w = make_weights(cfg, LV2_SEED, per_tensor=True, embed_std=0.05)
+    w = lv2_decode_weights(cfg, LV2_SEED)
     short, lf = lv2_features()
     prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
-    for dt, tag in ((torch.float32, "f32"), (torch.float16, "f16")):
+    B = short.shape[0]
+    # LV2_TAGS=f16 (say): only those arithmetics (parallel processes; main() then writes lv2_decode.<tags>.npz, and
+    # `make_golden.py lv2_merge` joins the parts into lv2_decode.npz)
+    tags = os.environ.get("LV2_TAGS", "f32,f16,b16").split(",")
+    for dt, tag in ((torch.float32, "f32"), (torch.float16, "f16"), (torch.float32, "b16")):
+        if tag not in tags:
+            continue
         m = hf_model(cfg, w, dt).eval()
+        amp = torch.autocast("cpu", dtype=torch.bfloat16) if tag == "b16" else contextlib.nullcontext()
         feats = torch.from_numpy(short).to(dt)
-        m.generation_config = GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
-                                               pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
-                                               begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=448,
-                                               num_beams=1, do_sample=False,
-                                               no_timestamps_token_id=SPECIAL["notimestamps"])
+        m.generation_config = lv2_greedy_config()
         spy = _MarginSpy()
-        with torch.no_grad():
-            out[f"{tag}_greedy_ids"] = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * 2), max_new_tokens=48,
-                                                  logits_processor=LogitsProcessorList([spy])).numpy()
+        with torch.no_grad(), amp:
+            out[f"{tag}_greedy_ids"] = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * B),
+                                                  max_new_tokens=48, logits_processor=LogitsProcessorList([spy])).numpy()
         out[f"{tag}_greedy_margin"] = np.stack(spy.steps)
         m.generation_config = ts_generation_config()
-        spy = _MarginSpy()
-        with torch.no_grad():
-            out[f"{tag}_ts_ids"] = m.generate(feats, return_timestamps=True, language="zh", task="transcribe",
-                                              max_new_tokens=48, logits_processor=LogitsProcessorList([spy])).numpy()
-        out[f"{tag}_ts_margin"] = np.stack(spy.steps)
+        # one clip per call: HF's timestamp path drops finished rows from its batch (_maybe_reduce_batch), so a
+        # batched call's per-step margins cannot be mapped back to clips; rows are padded with -1 / nan
+        ids_l, mar_l = [], []
+        for b in range(B):
+            spy = _MarginSpy()
+            with torch.no_grad(), amp:
+                ids_l.append(m.generate(feats[b:b + 1], return_timestamps=True, language="zh", task="transcribe",
+                                        max_new_tokens=48, logits_processor=LogitsProcessorList([spy])).numpy()[0])
+            mar_l.append(np.concatenate([s_.reshape(-1) for s_ in spy.steps]))
+        L_ = max(len(x) for x in ids_l)
+        out[f"{tag}_ts_ids"] = np.stack([np.pad(x, (0, L_ - len(x)), constant_values=-1) for x in ids_l])
+        S_ = max(len(x) for x in mar_l)
+        out[f"{tag}_ts_margin"] = np.stack([np.pad(x, (0, S_ - len(x)), constant_values=np.nan) for x in mar_l]).T
+        print(tag, "greedy + timestamps done", flush=True)
         if tag == "f32":
-            lt = torch.from_numpy(lf)
+            lt = torch.from_numpy(lf).to(dt)
             kw = dict(attention_mask=torch.ones(1, lt.shape[-1], dtype=torch.long), return_timestamps=True,
                       language="zh", task="transcribe")
-            rec = {"avg": [], "ns": []}
+            rec = {"avg": [], "ns": [], "steps": []}
             orig_need = type(m)._need_fallback
 
             def need_spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
                          temperature):
+                rec["steps"].append(len(seek_outputs[index]["scores"]))
                 rec["avg"].append(float(self._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence,
                                                                     temperature)))
                 from transformers.generation.logits_process import WhisperNoSpeechDetection
@@ -486,14 +515,20 @@ def gen_lv2_decode(out):
                 return orig_need(self, seek_sequence, seek_outputs, index, logits_processor, generation_config,
                                  vocab_size, temperature)
             type(m)._need_fallback = need_spy
+            spy = _MarginSpy()
             try:
                 with torch.no_grad():
-                    out["f32_long_ids"] = m.generate(lt, temperature=(0.0,), logprob_threshold=-1e9,
-                                                     no_speech_threshold=1.0, **kw).numpy()
+                    out[f"{tag}_long_ids"] = m.generate(lt, temperature=(0.0,), logprob_threshold=-1e9,
+                                                        no_speech_threshold=1.0,
+                                                        logits_processor=LogitsProcessorList([spy]), **kw).numpy()
             finally:
                 type(m)._need_fallback = orig_need
-            out["f32_long_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
-            out["f32_long_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
+            out[f"{tag}_long_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
+            out[f"{tag}_long_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
+            out[f"{tag}_long_window_steps"] = np.array(rec["steps"], dtype=np.int64)
+            # one row per decode step over both windows, in order (batch of one)
+            out[f"{tag}_long_margin"] = np.concatenate([s_.reshape(-1) for s_ in spy.steps])
+            print(tag, "long-form done", flush=True)
         del m
     out["prompt"] = np.array(prompt)
     out["seed"] = np.int64(LV2_SEED)
@@ -645,9 +680,28 @@ def main():
             continue
         out = {}
         fn(out)
+        if name == "lv2_decode" and os.environ.get("LV2_TAGS"):
+            name = f"lv2_decode.{os.environ['LV2_TAGS'].replace(',', '_')}"
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
         print(name, {k: getattr(v, "shape", None) for k, v in list(out.items())[:12]})
 
 
+def lv2_merge():
+    """Join the lv2_decode.<tags>.npz parts (LV2_TAGS runs) into lv2_decode.npz and remove them."""
+    import glob
+    out = {}
+    parts = sorted(glob.glob(os.path.join(HERE, "lv2_decode.*.npz")))
+    for p_ in parts:
+        z = np.load(p_)
+        out.update({k: z[k] for k in z.files})
+    np.savez_compressed(os.path.join(HERE, "lv2_decode.npz"), **out)
+    for p_ in parts:
+        os.remove(p_)
+    print("lv2_decode", sorted(out))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["lv2_merge"]:
+        lv2_merge()
+    else:
+        main()
