@@ -340,8 +340,15 @@ class _BeamDecoder:
     can beat the worst kept hypothesis (early_stopping False: the heuristic at the current length) or every
     candidate hits max_length."""
 
-    def __init__(self, model, gc, B, nb, Tk, P, max_length):
+    def __init__(self, model, gc, B, nb, Tk, P, max_length, timestamps=None):
         self.m, self.gc, self.B, self.nb, self.Tk, self.P, self.T_max = model, gc, B, nb, Tk, P, max_length
+        # timestamps: (ts_begin, no_ts, max_initial) -> HF WhisperTimeStampLogitsProcessor on the log-probs after the
+        # suppress processors (generation_whisper.py _retrieve_logit_processors order), begin_index = P; with it the
+        # decoder also tracks, per hypothesis, the sum over its steps of log_softmax(processed row)[token] -- what HF's
+        # _retrieve_avg_logprobs sums over the chosen beam's scores (beam_indices) for the fallback gate
+        self.ts = timestamps
+        self.sum_logp = None      # [B] after run(): that sum for each clip's best hypothesis
+        self.ns_prob = None       # [B] after run(no_speech=...): no-speech probability (_ns)
         dev = model.device
         self.V = model.config.vocab_size
         self.eos = int(gc.eos_token_id)
@@ -354,6 +361,12 @@ class _BeamDecoder:
         es = getattr(gc, "early_stopping", False)
         self.early_stopping = False if es is None else es
 
+    def _ns(self, sess, token):
+        """WhisperNoSpeechDetection under beam search (is_scores_logprobs): exp of the fp32 log-softmax of the raw
+        logits at <|startoftranscript|>, the first beam row of each clip (every beam row holds the prompt there)."""
+        lg = sess.logits.view(self.B, self.nb, -1)[:, 0, :self.V].float()
+        return torch.log_softmax(lg, dim=-1)[:, token].exp()
+
     @staticmethod
     def _gather(t, idx):
         """HF _gather_beams: t [B, K, ...] rows picked per clip by idx [B, k]."""
@@ -361,8 +374,43 @@ class _BeamDecoder:
             idx = idx.unsqueeze(-1)
         return torch.gather(t, 1, idx.expand(*idx.shape[:2], *t.shape[2:]))
 
-    def run(self, enc16, prompt):
-        """enc16: [B*Tk, d] encoder rows; prompt: int64 [P] (device or host) -> generated ids [B, L] (device)."""
+    def _ts_rules(self, logp, run_seq, run_last_ts, cur):
+        """HF WhisperTimeStampLogitsProcessor (transformers generation/logits_process.py) on the B*k processed
+        log-prob rows, vectorised: <|notimestamps|> masked; timestamps in pairs (after a pair no timestamp, after a single
+        one no text); timestamps never decrease (nor repeat <|0.00|>); the first step a timestamp <= max_initial; then
+        text masked where the timestamps' summed probability beats every text token."""
+        tb, no_ts, max_initial = self.ts
+        eos = self.eos
+        BN, V = logp.shape
+        logp[:, no_ts] = -float("inf")
+        ngen = cur - self.P
+        cols = torch.arange(V, device=logp.device)
+        if ngen >= 1:
+            last = run_seq[:, :, cur - 1].reshape(-1)
+            last_is = last >= tb
+            pen_is = (run_seq[:, :, cur - 2].reshape(-1) >= tb) if ngen >= 2 else torch.ones_like(last_is)
+            kill_ts = last_is & pen_is
+            kill_text = last_is & ~pen_is
+            logp.masked_fill_(kill_ts[:, None] & (cols >= tb)[None, :], -float("inf"))
+            logp.masked_fill_(kill_text[:, None] & (cols < eos)[None, :], -float("inf"))
+            lts = run_last_ts.reshape(-1)
+            lim = torch.where(kill_text, lts, lts + 1)
+            logp.masked_fill_((lts >= 0)[:, None] & (cols >= tb)[None, :] & (cols[None, :] < lim[:, None]),
+                              -float("inf"))
+        else:
+            logp[:, :tb] = -float("inf")
+            if max_initial is not None:
+                logp[:, tb + max_initial + 1:] = -float("inf")
+        lp2 = torch.log_softmax(logp.float(), dim=-1)
+        ts_mass = torch.logsumexp(lp2[:, tb:], dim=-1)
+        text_max = lp2[:, :tb].max(dim=-1).values
+        logp.masked_fill_((ts_mass > text_max)[:, None] & (cols < tb)[None, :], -float("inf"))
+        return logp
+
+    def run(self, enc16, prompt, no_speech=None):
+        """enc16: [B*Tk, d] encoder rows; prompt: int64 [P] (device or host) -> generated ids [B, L] (device).
+        no_speech = (sot_position, token): softmax of the raw logits at that prompt position for that token goes to
+        self.ns_prob (WhisperNoSpeechDetection)."""
         m, B, nb, P, T_max, V = self.m, self.B, self.nb, self.P, self.T_max, self.V
         dev = m.device
         d = m.config.d_model
@@ -372,10 +420,13 @@ class _BeamDecoder:
         sess = DecodeSession(m, enc_rep, BN, self.Tk, T_max)
         del enc_rep
         sess.t_dev.zero_()
+        pl = prompt.tolist()                                     # one host read for the whole prompt
         for t in range(P - 1):                                   # prompt prefill (identical on every row)
-            sess.cur.fill_(int(prompt[t]))
+            sess.cur.fill_(pl[t])
             sess.step()
-        sess.cur.fill_(int(prompt[P - 1]))
+            if no_speech is not None and t == no_speech[0]:
+                self.ns_prob = self._ns(sess, no_speech[1])
+        sess.cur.fill_(pl[P - 1])
         K = max(2, 2) * nb                                       # beams_to_keep: (1 eos token + 1) * k
         top_mask = torch.zeros(K, dtype=torch.bool, device=dev)
         top_mask[:nb] = True
@@ -390,19 +441,34 @@ class _BeamDecoder:
         run_bidx = torch.full((B, nb, T_max - P), -1, dtype=torch.int32, device=dev)
         bidx = run_bidx.clone()
         lp, es = self.length_penalty, self.early_stopping
+        rows_ident = torch.arange(BN, dtype=torch.int64, device=dev)
+        ts = self.ts is not None
+        run_last_ts = torch.full((B, nb), -1, dtype=torch.int64, device=dev)     # last timestamp token per beam
+        run_sum = torch.zeros(B, nb, dtype=torch.float32, device=dev)            # sum of renormalised log-probs
+        fin_sum = torch.zeros(B, nb, dtype=torch.float32, device=dev)
         cur = P
         while True:
             sess.step()                                          # logits of position cur - 1 on every row
+            if no_speech is not None and cur == P and no_speech[0] == P - 1:
+                self.ns_prob = self._ns(sess, no_speech[1])
             logp = torch.log_softmax(sess.logits[:, :V].float(), dim=-1)
             if self.sup.numel():
                 logp[:, self.sup] = -float("inf")
             if cur == P and self.beg.numel():                    # SuppressTokensAtBegin (begin_index = P)
                 logp[:, self.beg] = -float("inf")
+            if ts:
+                logp = self._ts_rules(logp, run_seq, run_last_ts, cur)
             acc = (logp.view(B, nb, V) + run_scores[:, :, None]).reshape(B, nb * V)
             # _get_top_k_continuations
             top_lp, top_i = torch.topk(acc, k=K)
             src = top_i // V
             tok = top_i % V
+            if ts:
+                # HF's gate sums log_softmax(processed row)[token] along the chosen beam: processed - lse(processed)
+                lse = torch.logsumexp(logp, dim=-1).view(B, nb)
+                contrib = torch.gather(logp.view(B, nb * V), 1, top_i) - torch.gather(lse, 1, src)
+                top_sum = torch.gather(run_sum, 1, src) + contrib
+                top_last_ts = torch.where(tok >= self.ts[0], tok, torch.gather(run_last_ts, 1, src))
             top_bidx = self._gather(run_bidx, src)
             top_seq = self._gather(run_seq, src)
             top_seq[:, :, cur] = tok
@@ -415,6 +481,9 @@ class _BeamDecoder:
             run_seq = self._gather(top_seq, nxt)
             run_scores = self._gather(run_lp, nxt)
             run_bidx = self._gather(top_bidx, nxt)
+            if ts:
+                run_sum = self._gather(top_sum, nxt)
+                run_last_ts = self._gather(top_last_ts, nxt)
             # _update_finished_beams
             just = hits & top_mask[None, :]
             fin_lp = top_lp / ((cur + 1 - P) ** lp)
@@ -429,10 +498,10 @@ class _BeamDecoder:
             keep = torch.topk(m_sc, k=nb)[1]
             seqs, scores = self._gather(m_seq, keep), self._gather(m_sc, keep)
             bidx, finished = self._gather(m_bi, keep), self._gather(m_fin, keep)
-            # the next step's inputs: caches gathered by each running beam's source row, its new token
+            if ts:
+                fin_sum = self._gather(torch.cat((fin_sum, top_sum), 1), keep)
+            # the next step's inputs: each running beam's new token, its source row's caches
             src_rows = run_bidx[:, :, cur - P].reshape(-1).to(torch.int64)
-            for c in sess.self_kv:
-                c[:, :cur].copy_(c[:, :cur].index_select(0, src_rows))
             sess.cur.copy_(run_seq[:, :, cur].reshape(-1))
             cur += 1
             # _check_early_stop_heuristic / _beam_search_has_unfinished_sequences
@@ -443,12 +512,20 @@ class _BeamDecoder:
             best_run = run_scores[:, :1] / (best_len ** lp)
             worst_fin = torch.where(finished, torch.min(scores, dim=1, keepdim=True)[0], torch.full_like(scores, -1e9))
             heur_unsat = heur_unsat & torch.any(best_run > worst_fin, dim=-1, keepdim=True)
-            go = bool(torch.any(heur_unsat)) and not (bool(torch.all(finished)) and es is True) and \
-                not bool(torch.all(hits))
+            # one host read per step for every decision: continue?  and is the beam reorder the identity (every
+            # running beam continues its own row), in which case the cache gather is skipped
+            flags = torch.stack([torch.any(heur_unsat), torch.all(finished), torch.all(hits),
+                                 (src_rows == rows_ident).all()]).tolist()
+            go = flags[0] and not (flags[1] and es is True) and not flags[2]
             if not go or cur >= T_max:
                 break
+            if not flags[3]:
+                for c in sess.self_kv:
+                    c[:, :cur - 1].copy_(c[:, :cur - 1].index_select(0, src_rows))
         best = seqs[:, 0]
         gen_len = int(((bidx[:, 0] + 1) != 0).sum(dim=1).max())
+        if ts:
+            self.sum_logp = fin_sum[:, 0]
         return best[:, P:P + gen_len]
 
 
@@ -492,10 +569,6 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
              use_graph=None, **kw):
     from .config import GenerationConfig
     nb = 1 if num_beams is None else int(num_beams)
-    if nb > 1 and (return_timestamps or (input_features is not None and input_features.shape[-1] >
-                                          2 * model.config.max_source_positions)):
-        raise NotImplementedError("tw generate: beam search is built for short-form decoding without timestamps "
-                                  "(run_eval.py --num_beams / generation_num_beams at the reference's defaults)")
     temperature = kw.get("temperature")
     fb = dict(temperature=temperature if temperature is not None else 0.0,
               compression_ratio_threshold=kw.get("compression_ratio_threshold"),
@@ -515,7 +588,8 @@ def generate(model, input_features=None, max_length=None, num_beams=1, return_ti
     seek_loop = bool(return_timestamps) and decoder_input_ids is None
     if encoder_outputs is None and input_features is not None and (input_features.shape[-1] > window or seek_loop):
         return _longform(model, gc, input_features, attention_mask, language, task, max_length, max_new_tokens,
-                         use_graph, window, kw.get("_trace"), fallback_batch=bool(kw.get("fallback_batch", True)), **fb)
+                         use_graph, window, kw.get("_trace"), fallback_batch=bool(kw.get("fallback_batch", True)),
+                         num_beams=nb, **fb)
     if kw.get("do_sample") or fb["temperature"] not in (0, 0.0) or fb["logprob_threshold"] is not None \
             or fb["compression_ratio_threshold"] is not None or fb["no_speech_threshold"] is not None:
         # the reference applies fallback / thresholds to long-form inputs only (run_eval.py:659-685)
@@ -590,7 +664,7 @@ def need_fallback(tokens, avg_logprob, no_speech_prob, vocab_size, compression_r
 
 def _longform(model, gc, feats, attention_mask, language, task, max_length, max_new_tokens, use_graph, window,
               trace=None, temperature=0.0, compression_ratio_threshold=None, logprob_threshold=None,
-              no_speech_threshold=None, condition_on_prev_tokens=False, seed=0, fallback_batch=True):
+              no_speech_threshold=None, condition_on_prev_tokens=False, seed=0, fallback_batch=True, num_beams=1):
     """HF sequential long-form generate (generation_whisper.py step 6): per input, 30 s windows from
     `seek`; each window decoded with timestamp rules at the first temperature of `temperature` and
     re-decoded at the next one while HF's fallback test fails (compression ratio of the token bytes,
@@ -604,7 +678,9 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
     softmax(x / T) with the engine's counter-based RNG (seeded by `seed`, the clip, the window and
     the fallback index), not torch's RNG stream.  Once a window's first attempt fails, the remaining
     temperatures are decoded together as one batch (fallback_batch; identical tokens and gates to decoding
-    them one by one, see the loop below)."""
+    them one by one, see the loop below).  num_beams > 1 (run_eval.py --num_beams with timestamps / long-form): as HF
+    generate_with_fallback, a temperature-0 attempt is a beam search over the window (_BeamDecoder with the timestamp
+    rules; its gates from the chosen hypothesis's per-step processed scores), a sampled attempt keeps one beam."""
     cfg = model.config
     dev = model.device
     feats = feats.to(dev, torch.float32)
@@ -649,7 +725,10 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
     # the per-clip loop below takes them over and continues (fallback attempts, later windows) clip by clip.
     first = {}
     live = [b for b in range(B) if int(lens[b]) > 0]
-    if len(live) > 1 and batch_rows_independent(model):
+    nbeam = max(1, int(num_beams or 1))
+    beam_ts = (ts_begin, int(gc.no_timestamps_token_id), gc.max_initial_timestamp_index
+               if "max_initial_timestamp_index" in gc else None)
+    if len(live) > 1 and batch_rows_independent(model) and nbeam == 1:
         P0 = len(init)
         ml0 = total_length(cfg, gc, P0, max_length, max_new_tokens)
         ns0 = (0, ns_token) if no_speech_threshold is not None else None
@@ -711,14 +790,23 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
             attempts = [(0, dec, enc16, ptens, [temps[0] or 0.0], [seeds[0]])]
             rest = list(range(1, len(temps)))
             # fallback_batch=False: one attempt at a time (A/B, tests); so does the fp32 compute path, whose rows are
-            # not shown independent of the batch (batch_rows_independent)
+            # not shown independent of the batch (batch_rows_independent), and a beam search at temperature 0 later
+            # in the schedule
             per = 8 if fallback_batch and batch_rows_independent(model) else 1
+            if nbeam > 1 and any(not temps[f] for f in rest):
+                per = 1
             for fb in range(0, len(rest), per):
                 grp = rest[fb:fb + per]
                 attempts.append((grp[0], None, None, None, [temps[f] or 0.0 for f in grp], [seeds[f] for f in grp]))
             for fi0, d_, e_, p_, tl, sl in attempts:
                 if fi0 == 0 and pre is not None:             # attempt 0 ran in the first-window batch
                     raws, gates, nbatch = [pre[0]], [(pre[1], pre[2])], pre[4]
+                elif nbeam > 1 and len(tl) == 1 and not tl[0]:   # temperature 0 with num_beams: the beam search
+                    bd = _BeamDecoder(model, gc, 1, nbeam, cfg.max_source_positions, P, ml, timestamps=beam_ts)
+                    raw = row_tokens(bd.run(enc16, prompt, no_speech=ns)[0].tolist(), eos)
+                    avg = float(bd.sum_logp[0]) / max(len(trim(raw)), 1)
+                    nsp = float(bd.ns_prob[0]) if ns is not None else 0.0
+                    raws, gates, nbatch = [raw], [(avg, nsp)], 1
                 else:
                     if d_ is None:                           # a speculative batch of the remaining attempts
                         nb = len(tl)
@@ -736,7 +824,7 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                     fi, temp = fi0 + r, temps[fi0 + r]
                     cand = trim(raw)
                     needs = False
-                    if track or compression_ratio_threshold is not None:
+                    if track or compression_ratio_threshold is not None or (nbeam > 1 and gates is not None):
                         tg = time.perf_counter()      # gate cost: log-prob / no-speech readback + compression ratio
                         if gates is not None:
                             avg, nsp = gates[r]

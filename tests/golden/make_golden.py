@@ -270,6 +270,51 @@ def gen_beam(out):
     out["beam_eos_scale"] = np.float32(6.0)
 
 
+def gen_beam_ts(out):
+    """HF `generate(num_beams=k, return_timestamps=True)` on the timestamp fixtures' micro model (lin_std 0.2): the
+    seek loop with a beam search per window (generate_with_fallback: the temperature-0 attempt keeps num_beams), the
+    timestamp processor on the log-probs, HF's beam _postprocess_outputs (the chosen beam's per-step scores through
+    beam_indices) for the gates.
+      bts{k}_short_ids : 2 clips <= 30 s, language zh, max_new_tokens 48
+      bts{k}_long_ids, bts{k}_long_avg_logprobs, bts{k}_long_ns_probs : the 65 s input, temperature (0.0,), thresholds
+                         that never fire (logprob -1e9, no-speech 1.0), per-window gates recorded in _need_fallback"""
+    cfg = CONFIGS["micro"]
+    m = hf_model(cfg, make_weights(cfg, 1, lin_std=0.2)).eval()
+    feats = torch.from_numpy(logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(2, 9.0)]))
+    lf = torch.from_numpy(longform_features())
+    am = torch.ones(1, lf.shape[-1], dtype=torch.long)
+    for k in (2, 4):
+        m.generation_config = ts_generation_config()
+        with torch.no_grad():
+            out[f"bts{k}_short_ids"] = m.generate(feats, return_timestamps=True, language="zh", task="transcribe",
+                                                  max_new_tokens=48, num_beams=k).numpy()
+        rec = {"avg": [], "ns": []}
+        orig_need = type(m)._need_fallback
+
+        def spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
+                temperature):
+            rec["avg"].append(float(self._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence,
+                                                                temperature)))
+            from transformers.generation.logits_process import WhisperNoSpeechDetection
+            for p_ in logits_processor or []:
+                if isinstance(p_, WhisperNoSpeechDetection):
+                    rec["ns"].append(float(p_.no_speech_prob[index]))
+            return orig_need(self, seek_sequence, seek_outputs, index, logits_processor, generation_config,
+                             vocab_size, temperature)
+        m.generation_config = ts_generation_config()
+        type(m)._need_fallback = spy
+        try:
+            with torch.no_grad():
+                out[f"bts{k}_long_ids"] = m.generate(lf, attention_mask=am, return_timestamps=True, language="zh",
+                                                     task="transcribe", num_beams=k, temperature=(0.0,),
+                                                     logprob_threshold=-1e9, no_speech_threshold=1.0).numpy()
+        finally:
+            type(m)._need_fallback = orig_need
+        out[f"bts{k}_long_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
+        out[f"bts{k}_long_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
+        print("beam_ts", k, "done", flush=True)
+
+
 def ts_generation_config():
     from transformers import GenerationConfig
     return GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
@@ -671,7 +716,7 @@ def gen_cfg(case, out):
 def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
-    for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy), ("beam", gen_beam),
+    for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy), ("beam", gen_beam), ("beam_ts", gen_beam_ts),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
                      ("lv2_decode", gen_lv2_decode),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
