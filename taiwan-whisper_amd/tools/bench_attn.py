@@ -10,6 +10,7 @@ from tw import ops
 
 def main():
     dev = "cuda"
+    torch.manual_seed(0)
     B, H = 64, 20
     d = H * 64
     for name, Tq, Tk, causal in (("enc self", 1500, 1500, False), ("dec self", 447, 447, True),
@@ -32,7 +33,8 @@ def main():
             ts.append(e0.elapsed_time(e1) / 3)
         t = sorted(ts)[2]
         fl = 4.0 * B * H * Tq * Tk * 64 * (0.5 if causal else 1.0)
-        print(f"fwd {name:9s} {t*1e3:8.1f}us {fl/t/1e9:7.1f} TF/s (causal counted at half)", flush=True)
+        csum = int(o.view(torch.int16).to(torch.int64).sum()) ^ int(lse.view(torch.int32).to(torch.int64).sum())
+        print(f"fwd {name:9s} {t*1e3:8.1f}us {fl/t/1e9:7.1f} TF/s (causal counted at half)  bits {csum}", flush=True)
         do = torch.randn(B * Tq, d, device=dev).bfloat16()
         dq = torch.empty(B * Tq, d, dtype=torch.bfloat16, device=dev)
         dkv = torch.empty(B * Tk, 2 * d, dtype=torch.bfloat16, device=dev)
