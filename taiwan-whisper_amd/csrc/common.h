@@ -200,6 +200,76 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- the same butterflies on the VALU (DPP row rotations / mirrors, v_permlane16/32_swap) instead of ds_bpermute
+// round trips.  Each keeps the xor pairing order of the __shfl_xor form it replaces; where a rotation reaches a lane
+// other than the xor partner, that lane already holds the partner's value (the earlier steps made the lanes of each
+// merged class equal), and IEEE addition is commutative, so the results are bit-identical.
+#define TW_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), (ctrl), 0xf, 0xf, false))
+#define TW_ROW_ROR(n) (0x120 + (n))
+#define TW_QUAD_XOR1 0xB1          // quad_perm [1,0,3,2]
+#define TW_QUAD_XOR2 0x4E          // quad_perm [2,3,0,1]
+#define TW_ROW_HALF_MIRROR 0x141   // lane i <-> 7 - i within each 8 (xor 4 once the quads are merged)
+__device__ __forceinline__ float swap32_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float swap16_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+// wave_sum: xor 32, 16, 8, 4, 2, 1
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = swap32_sum(v);
+  v = swap16_sum(v);
+  v += TW_DPP(v, TW_ROW_ROR(8));
+  v += TW_DPP(v, TW_ROW_ROR(4));
+  v += TW_DPP(v, TW_ROW_ROR(2));
+  v += TW_DPP(v, TW_ROW_ROR(1));
+  return v;
+}
+// xor 1, 2, 4 (a sum over each 8-lane group)
+__device__ __forceinline__ float oct_sum_dpp(float v) {
+  v += TW_DPP(v, TW_QUAD_XOR1);
+  v += TW_DPP(v, TW_QUAD_XOR2);
+  v += TW_DPP(v, TW_ROW_HALF_MIRROR);
+  return v;
+}
+// xor 8, 16, 32 (a sum over the lanes with equal lane & 7)
+__device__ __forceinline__ float stride8_sum_dpp(float v) {
+  v += TW_DPP(v, TW_ROW_ROR(8));
+  v = swap16_sum(v);
+  return swap32_sum(v);
+}
+// xor 16, 8, 4, 2, 1 (a sum over each 32-lane half)
+__device__ __forceinline__ float half_sum_dpp(float v) {
+  v = swap16_sum(v);
+  v += TW_DPP(v, TW_ROW_ROR(8));
+  v += TW_DPP(v, TW_ROW_ROR(4));
+  v += TW_DPP(v, TW_ROW_ROR(2));
+  v += TW_DPP(v, TW_ROW_ROR(1));
+  return v;
+}
+// lane c's value (c wave-uniform); the builtin is int-typed, so the bits go through as an int
+__device__ __forceinline__ float readlane_f(float v, int c) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), c));
+}
+// wave_max (max is order-independent)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  }
+  {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  }
+  v = fmaxf(v, TW_DPP(v, TW_ROW_ROR(8)));
+  v = fmaxf(v, TW_DPP(v, TW_ROW_ROR(4)));
+  v = fmaxf(v, TW_DPP(v, TW_ROW_ROR(2)));
+  v = fmaxf(v, TW_DPP(v, TW_ROW_ROR(1)));
+  return v;
+}
+
 // raw buffer descriptor: out-of-range per-lane offsets (>= num_records) read as zero.
 #define TW_OOB 0x80000000u
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {

@@ -82,9 +82,7 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
 #pragma unroll
         for (int j = 0; j < 8; ++j) sv = fmaf(qv[j], t[u][j], sv);
       }
-      sv += __shfl_xor(sv, 1, 64);
-      sv += __shfl_xor(sv, 2, 64);
-      sv += __shfl_xor(sv, 4, 64);
+      sv = oct_sum_dpp(sv);          // xor 1, 2, 4 on the VALU (bit-identical to the shuffles: common.h)
       if (key < hi) {
         sv *= p.c;
         if (ch == 0) sc[key - lo] = sv;
@@ -92,7 +90,7 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
       }
     }
   }
-  mx = wave_max(mx);
+  mx = wave_max_dpp(mx);
   if (lane == 0) red_m[wave] = mx;
   __syncthreads();
   float m = red_m[0];
@@ -121,12 +119,8 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
   }
   // reduce over the 8 key slots of the wave (lanes ch, ch+8, ..., ch+56), then over waves
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    o[j] += __shfl_xor(o[j], 8, 64);
-    o[j] += __shfl_xor(o[j], 16, 64);
-    o[j] += __shfl_xor(o[j], 32, 64);
-  }
-  l = wave_sum(l);
+  for (int j = 0; j < 8; ++j) o[j] = stride8_sum_dpp(o[j]);    // xor 8, 16, 32
+  l = wave_sum_dpp(l);
   if (ks == 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[wave][ch * 8 + j] = o[j];
@@ -165,14 +159,14 @@ __device__ __forceinline__ void combine_row(const DecP& p, int bh, int nchunk, c
   float oc[DA_MAX_CHUNK];
 #pragma unroll
   for (int c = 0; c < DA_MAX_CHUNK; ++c) oc[c] = c < nchunk ? part[c * 66 + lane] : 0.f;
-  const float M = wave_max(mc);
+  const float M = wave_max_dpp(mc);
   const float wc = mc == -INFINITY ? 0.f : (sizeof(E) == 4 ? exp2f(mc - M) : __builtin_amdgcn_exp2f(mc - M));
   float acc = 0.f, lt = 0.f;
 #pragma unroll
   for (int c = 0; c < DA_MAX_CHUNK; ++c) {
     if (c < nchunk) {
-      const float w = __shfl(wc, c, 64), l = __shfl(lc, c, 64);
-      if (__shfl(mc, c, 64) != -INFINITY) {
+      const float w = readlane_f(wc, c), l = readlane_f(lc, c);
+      if (readlane_f(mc, c) != -INFINITY) {
         acc = fmaf(w, oc[c], acc);
         lt = fmaf(w, l, lt);
       }

@@ -47,6 +47,11 @@ struct GemvKV {
   const int* t;
 };
 
+// one 16-B piece of a weight row, a non-temporal load: the decode step streams each weight once per step (1.5 GB per
+// large-v2 step, far past the 256 MiB Infinity Cache), so nothing is gained by keeping it; the nt policy cut the
+// batch-1 large-v2 fp16 step from 2.18 to 2.01 ms (tools/bench_step.py, profiles/r05_j_gemv_variants_ab.log)
+__device__ __forceinline__ bf16x8 ldw8(const bf16* q) { return __builtin_nontemporal_load((const bf16x8*)q); }
+
 // the first PRE 16-B pieces per lane of W rows n0 .. n0 + CPW - 1 (rows past N read row 0, never stored)
 template <bool H, int CPW, int PRE>
 __device__ __forceinline__ void gemv_preload(const GemmP& p, int n0, int lane, bf16x8 (&wpre)[CPW][PRE]) {
@@ -56,7 +61,7 @@ __device__ __forceinline__ void gemv_preload(const GemmP& p, int n0, int lane, b
     const int n = n0 + c;
     const bf16* wr = p.B + (int64_t)(n < p.N ? n : 0) * p.ldb;
 #pragma unroll
-    for (int u = 0; u < PRE; ++u) wpre[c][u] = (u < npre) ? *(const bf16x8*)(wr + lane * 8 + u * 512) : bf16x8{};
+    for (int u = 0; u < PRE; ++u) wpre[c][u] = (u < npre) ? ldw8(wr + lane * 8 + u * 512) : bf16x8{};
   }
 }
 
@@ -66,6 +71,73 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
                                                 const float* __restrict__ lnb, float eps, bf16* xs, int wave, int nw,
                                                 int lane) {
   const int K = p.K;
+  if (MR > 1 && lnw && K <= 1280) {
+    // batches of 2..8 rows: one global pass -- every row of this wave (rows wave, wave + nw, ...) and the LN
+    // parameters loaded to registers at once, then the same half-wave statistics in the same order as below
+    // (bit-identical A).  At MR = 1 the three-pass form measured faster (profiles/r05_j_gemv_variants_ab.log)
+    constexpr int RPW = (MR + 3) / 4;
+    const int hl = lane & 31, nch = K / 256;
+    bf16x8 t[RPW][5];
+    f32x4 wv[5][2], bv[5][2];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = wave + j * nw;
+      const bf16* xr = p.A + (int64_t)(row < p.M ? row : 0) * p.lda;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) t[j][c] = c < nch ? *(const bf16x8*)(xr + (c * 32 + hl) * 8) : bf16x8{};
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const int e = (c * 32 + hl) * 8;
+      if (c < nch) {
+        wv[c][0] = *(const f32x4*)(lnw + e); wv[c][1] = *(const f32x4*)(lnw + e + 4);
+        bv[c][0] = *(const f32x4*)(lnb + e); bv[c][1] = *(const f32x4*)(lnb + e + 4);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = wave + j * nw;
+      if (row >= MR) break;
+      bf16* dst = xs + (int64_t)row * K;
+      if (row >= p.M) {
+        for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = bf16x8{};
+        continue;
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+        if (c < nch)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) s += e2f<H>(t[j][c][q]);
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      const float mean = s / K;
+      float ss = 0.f;
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+        if (c < nch)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[j][c][q]) - mean; ss += d * d; }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      const float rstd = rsqrtf(ss / K + eps);
+      if (lane < 32) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+          if (c < nch) {
+            bf16x8 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              o[q] = f2e<H>((e2f<H>(t[j][c][q]) - mean) * rstd * wv[c][0][q] + bv[c][0][q]);
+              o[q + 4] = f2e<H>((e2f<H>(t[j][c][q + 4]) - mean) * rstd * wv[c][1][q] + bv[c][1][q]);
+            }
+            *(bf16x8*)(dst + (c * 32 + hl) * 8) = o;
+          }
+        }
+      }
+    }
+    return;
+  }
   for (int row = wave; row < MR; row += nw) {
     bf16* dst = xs + (int64_t)row * K;
     if (row >= p.M) {
@@ -117,6 +189,26 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 }
 
 // columns n0 .. n0 + CPW - 1 against the staged rows (xs visible to this wave), then the epilogue by lane 0
+// acc = fma(w[q], a[q], acc) for q = 0..7 in order, the 16-bit operands widened exactly to fp32.  fp16: one
+// v_fma_mix_f32 per element (the f16 -> f32 widening inside the FMA: the same single rounding as fmaf on the widened
+// operands, without the 16 v_cvt_f32_f16 per 8 elements the compiler otherwise emits beside each row)
+typedef __attribute__((ext_vector_type(4))) unsigned int gv_u32x4;
+
+template <bool H>
+__device__ __forceinline__ void fma8(float& acc, const bf16x8& w, const bf16x8& a) {
+  if constexpr (H) {
+    const gv_u32x4 wu = __builtin_bit_cast(gv_u32x4, w), au = __builtin_bit_cast(gv_u32x4, a);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(wu[i]), "v"(au[i]));
+      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(wu[i]), "v"(au[i]));
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc = fmaf(e2f<H>(w[q]), e2f<H>(a[q]), acc);
+  }
+}
+
 template <bool H, int MR, int CPW, int PRE>
 __device__ __forceinline__ void gemv_finish(const GemmP& p, const GemvKV& kv, const bf16* xs, int n0, int lane,
                                             const bf16x8 (&wpre)[CPW][PRE]) {
@@ -135,9 +227,7 @@ __device__ __forceinline__ void gemv_finish(const GemmP& p, const GemvKV& kv, co
       for (int r = 0; r < MR; ++r) {
         const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + lane * 8 + u * 512);
 #pragma unroll
-        for (int c = 0; c < CPW; ++c)
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(e2f<H>(wpre[c][u][q]), e2f<H>(a8[q]), acc[c][r]);
+        for (int c = 0; c < CPW; ++c) fma8<H>(acc[c][r], wpre[c][u], a8);
       }
     }
   }
@@ -145,38 +235,38 @@ __device__ __forceinline__ void gemv_finish(const GemmP& p, const GemvKV& kv, co
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
       const int n = n0 + c;
-      const bf16x8 w8 = *(const bf16x8*)(p.B + (int64_t)(n < p.N ? n : 0) * p.ldb + k0);
+      const bf16x8 w8 = ldw8(p.B + (int64_t)(n < p.N ? n : 0) * p.ldb + k0);
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const bf16x8 a8 = *(const bf16x8*)(xs + (int64_t)r * K + k0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[c][r] = fmaf(e2f<H>(w8[q]), e2f<H>(a8[q]), acc[c][r]);
+        fma8<H>(acc[c][r], w8, a8);
       }
     }
   }
+  // every lane gets every (column, row) total; lane c * MR + r then runs the epilogue of (n0 + c, r), all outputs of
+  // the wave at once (the same per-element arithmetic as a single lane running them in turn)
+  float mine = 0.f;
 #pragma unroll
   for (int c = 0; c < CPW; ++c)
 #pragma unroll
-    for (int r = 0; r < MR; ++r) acc[c][r] = wave_sum(acc[c][r]);
-  if (lane == 0) {
-    const int64_t t = kv.cache ? (int64_t)*kv.t : 0;
-#pragma unroll
-    for (int c = 0; c < CPW; ++c)
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        const int n = n0 + c;
-        if (r < p.M && n < p.N) {
-          const float v = epi_value<H>(p, r, n, acc[c][r]);
-          const int64_t co = (int64_t)r * p.ldc + n;
-          if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
-          else ((float*)p.C)[co] = v;
-          if (kv.cache && n >= kv.col0) {
-            const int64_t ko = r * kv.sb + t * kv.ld + (n - kv.col0);
-            if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2e<H>(v);
-            else ((float*)kv.cache)[ko] = v;
-          }
-        }
-      }
+    for (int r = 0; r < MR; ++r) {
+      const float tot = wave_sum_dpp(acc[c][r]);
+      if (lane == c * MR + r) mine = tot;
+    }
+  static_assert(CPW * MR <= 64, "one output per lane");
+  const int c = lane / MR, r = lane % MR;
+  const int n = n0 + c;
+  if (c < CPW && r < p.M && n < p.N) {
+    const float v = epi_value<H>(p, r, n, mine);
+    const int64_t co = (int64_t)r * p.ldc + n;
+    if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
+    else ((float*)p.C)[co] = v;
+    if (kv.cache && n >= kv.col0) {
+      const int64_t t = (int64_t)*kv.t;
+      const int64_t ko = r * kv.sb + t * kv.ld + (n - kv.col0);
+      if (p.c_dtype == TW_BF16) ((bf16*)kv.cache)[ko] = f2e<H>(v);
+      else ((float*)kv.cache)[ko] = v;
+    }
   }
 }
 

@@ -708,6 +708,30 @@ def test_logmel_longform_matches_oracle_and_hf():
 
 
 # ----------------------------------------------------------------------------- decode GEMV
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,K,ln", [(1280, 1280, True), (3840, 1280, False), (1280, 5120, False)])
+def test_gemv_rows_independent_of_batch(dt, N, K, ln):
+    """Each row of an M-row GEMV (M = 2..8, the fallback batch of a long-form window) is bit-identical to the
+    same row decoded alone (M = 1): tw.generation.batch_rows_independent relies on it to decode the remaining
+    temperatures of a window as one batch.  Covers the fused LayerNorm, bias, GELU and residual epilogues."""
+    from tw import ops
+    g = torch.Generator().manual_seed(N + K)
+    x = (torch.randn(8, K, generator=g) * 2 + 0.3).to(dt).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dt).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(dt).to(DEV)
+    r = (torch.randn(8, N, generator=g)).to(dt).to(DEV)
+    lw, lb = (torch.randn(K, generator=g) * 0.2 + 1).to(DEV), (torch.randn(K, generator=g) * 0.1).to(DEV)
+    kw = dict(ln_w=lw, ln_b=lb) if ln and K <= 1280 else {}
+    for flags, res in ((ops.GEMM_ROUND, None), (ops.GEMM_ROUND | ops.GEMM_GELU, None), (ops.GEMM_ROUND, r)):
+        one = torch.empty(8, N, dtype=dt, device=DEV)
+        for i in range(8):
+            ops.gemv(x[i:i + 1], W, one[i:i + 1], bias=b, flags=flags, res=None if res is None else res[i:i + 1], **kw)
+        for M in range(2, 9):
+            C = torch.empty(M, N, dtype=dt, device=DEV)
+            ops.gemv(x[:M], W, C, bias=b, flags=flags, res=None if res is None else res[:M], **kw)
+            assert torch.equal(C, one[:M]), (M, flags, (C != one[:M]).sum().item())
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (2, 3840, 1280), (4, 1280, 5120), (3, 520, 256), (1, 51904, 1280)])
 def test_gemv_decode(M, N, K):
     """tw_gemv_bf16 (batch <= 4 decode Linears) vs an fp64 reference of the bf16 operands (fp32 accumulation
