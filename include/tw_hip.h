@@ -167,6 +167,14 @@ int tw_count_valid(const int64_t* labels, int64_t n, int* out, tw_stream_t strea
 int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v, int64_t ldv,
                    int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev, int head_dim,
                    float scale, int dtype, tw_stream_t stream);
+/* tw_decode_attn_hs: tw_decode_attn with head strides for K and V -- key j of head h at k + b*skb + h*hsk + j*ldk
+ * (v alike; tw_decode_attn is hsk = hsv = 64).  The head-major cross-attention K/V ([H][Tk][64] per clip:
+ * hsk = Tk*64, ldk = 64) of ONE clip serve every row of a batch with skb = svb = 0 (the temperature-fallback batch
+ * of one window: HF generate_with_fallback, generation_whisper.py; each row reads exactly the K/V of its batch-1
+ * decode). */
+int tw_decode_attn_hs(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, int64_t hsk,
+                      const void* v, int64_t ldv, int64_t svb, int64_t hsv, void* o, int64_t sob, int B, int H, int Tk,
+                      const int* tk_dev, int head_dim, float scale, int dtype, tw_stream_t stream);
 int tw_greedy_select(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,
                      const uint32_t* begin_bits, int apply_begin, int64_t eos, uint8_t* done, int64_t* ids,
                      int64_t ld_ids, int col, int64_t* next_ids, const int* t_dev, int begin_col, tw_stream_t stream);

@@ -706,20 +706,23 @@ extern "C" int tw_step_advance(int* t_dev, int by, hipStream_t stream) {
   return TW_OK;
 }
 
-extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v,
-                              int64_t ldv, int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev,
-                              int head_dim, float scale, int dtype, hipStream_t stream) {
+extern "C" int tw_decode_attn_hs(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, int64_t hsk,
+                                 const void* v, int64_t ldv, int64_t svb, int64_t hsv, void* o, int64_t sob, int B,
+                                 int H, int Tk, const int* tk_dev, int head_dim, float scale, int dtype,
+                                 hipStream_t stream) {
   if (head_dim != 64) return TW_EUNSUPPORTED;
   if (B <= 0 || H <= 0) return TW_OK;
   if ((!tk_dev && Tk <= 0) || Tk > DA_MAX_TK) return TW_EUNSUPPORTED;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) return TW_EINVAL;
-  if ((sqb | ldk | skb | ldv | svb) & 7) return TW_EINVAL;
+  if ((sqb | ldk | skb | ldv | svb | hsk | hsv) & 7) return TW_EINVAL;
+  if (skb < 0 || svb < 0 || hsk < 0 || hsv < 0) return TW_EINVAL;
   DecP p;
   if (dtype == TW_F32 && ((sqb | ldk | skb | ldv | svb) & 3)) return TW_EINVAL;
   p.q = q; p.sqb = sqb;
   p.k = k; p.ldk = ldk; p.skb = skb;
   p.v = v; p.ldv = ldv; p.svb = svb;
   p.o = o; p.sob = sob;
+  p.hsk = hsk; p.hsv = hsv;
   p.H = H; p.Tk = Tk; p.tk_dev = tk_dev; p.c = scale * 1.4426950408889634f;
   // few (clip, head) pairs (batch-1 long-form, small batches): split the keys into chunks of DA_SPLIT over
   // the grid's y dimension, then combine.  Measured (tools/bench_decode_attn.py, H = 20, Tk = 1500): B = 1
@@ -743,6 +746,13 @@ extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t
   else TW_LAUNCH_DT(dtype, decode_attn_u4_kernel, dim3(B * H), dim3(DA_THREADS), p);
   TW_CHECK_LAUNCH();
   return TW_OK;
+}
+
+extern "C" int tw_decode_attn(const void* q, int64_t sqb, const void* k, int64_t ldk, int64_t skb, const void* v,
+                              int64_t ldv, int64_t svb, void* o, int64_t sob, int B, int H, int Tk, const int* tk_dev,
+                              int head_dim, float scale, int dtype, hipStream_t stream) {
+  return tw_decode_attn_hs(q, sqb, k, ldk, skb, 64, v, ldv, svb, 64, o, sob, B, H, Tk, tk_dev, head_dim, scale, dtype,
+                           stream);
 }
 
 extern "C" int tw_greedy_select(const void* logits, int64_t ld, int logits_dtype, int B, int V, const uint32_t* suppress_bits,

@@ -15,6 +15,7 @@ struct DecP {
   const void* k; int64_t ldk, skb;
   const void* v; int64_t ldv, svb;
   void* o; int64_t sob;
+  int64_t hsk, hsv;   // head strides of K and V (64: heads side by side in a row; Tk*64: head-major blocks)
   int H, Tk;
   const int* tk_dev;  // nullable: effective Tk = *tk_dev + Tk (graph-captured decode steps)
   float c;        // scale * log2(e)
@@ -60,8 +61,8 @@ __device__ __forceinline__ void decode_attn_body(const DecP& p, int b, int h, in
   const int ks = lane >> 3, ch = lane & 7;
   constexpr bool F32 = sizeof(E) == 4;
   const E* qb = (const E*)p.q + b * p.sqb + h * 64 + ch * 8;
-  const E* kb = (const E*)p.k + b * p.skb + h * 64 + ch * 8;
-  const E* vb = (const E*)p.v + b * p.svb + h * 64 + ch * 8;
+  const E* kb = (const E*)p.k + b * p.skb + h * p.hsk + ch * 8;
+  const E* vb = (const E*)p.v + b * p.svb + h * p.hsv + ch * 8;
   float qv[8];
   load8(qb, qv);
   // pass 1: scores (log2 domain) -> LDS, running max.  A wave takes 8 keys x DA_U sub-steps per iteration

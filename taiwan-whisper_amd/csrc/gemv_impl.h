@@ -72,27 +72,18 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
                                                 int lane) {
   const int K = p.K;
   if (MR > 1 && lnw && K <= 1280) {
-    // batches of 2..8 rows: one global pass -- every row of this wave (rows wave, wave + nw, ...) and the LN
-    // parameters loaded to registers at once, then the same half-wave statistics in the same order as below
+    // batches of 2..8 rows: one global pass -- every row of this wave (rows wave, wave + nw, ...) loaded to
+    // registers at once, then the same half-wave statistics in the same order as below
     // (bit-identical A).  At MR = 1 the three-pass form measured faster (profiles/r05_j_gemv_variants_ab.log)
     constexpr int RPW = (MR + 3) / 4;
     const int hl = lane & 31, nch = K / 256;
     bf16x8 t[RPW][5];
-    f32x4 wv[5][2], bv[5][2];
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int row = wave + j * nw;
       const bf16* xr = p.A + (int64_t)(row < p.M ? row : 0) * p.lda;
 #pragma unroll
       for (int c = 0; c < 5; ++c) t[j][c] = c < nch ? *(const bf16x8*)(xr + (c * 32 + hl) * 8) : bf16x8{};
-    }
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      const int e = (c * 32 + hl) * 8;
-      if (c < nch) {
-        wv[c][0] = *(const f32x4*)(lnw + e); wv[c][1] = *(const f32x4*)(lnw + e + 4);
-        bv[c][0] = *(const f32x4*)(lnb + e); bv[c][1] = *(const f32x4*)(lnb + e + 4);
-      }
     }
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
@@ -125,11 +116,16 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
         for (int c = 0; c < 5; ++c) {
           if (c < nch) {
+            // LN parameters loaded here, not with the rows: held for every chunk they cost ~80 VGPRs, which at
+            // MR = 8 cut the waves per SIMD below what the wide Linears (fc1: 5 waves per SIMD) need
+            const int e = (c * 32 + hl) * 8;
+            const f32x4 w0 = *(const f32x4*)(lnw + e), w1 = *(const f32x4*)(lnw + e + 4);
+            const f32x4 b0 = *(const f32x4*)(lnb + e), b1 = *(const f32x4*)(lnb + e + 4);
             bf16x8 o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              o[q] = f2e<H>((e2f<H>(t[j][c][q]) - mean) * rstd * wv[c][0][q] + bv[c][0][q]);
-              o[q + 4] = f2e<H>((e2f<H>(t[j][c][q + 4]) - mean) * rstd * wv[c][1][q] + bv[c][1][q]);
+              o[q] = f2e<H>((e2f<H>(t[j][c][q]) - mean) * rstd * w0[q] + b0[q]);
+              o[q + 4] = f2e<H>((e2f<H>(t[j][c][q + 4]) - mean) * rstd * w1[q] + b1[q]);
             }
             *(bf16x8*)(dst + (c * 32 + hl) * 8) = o;
           }

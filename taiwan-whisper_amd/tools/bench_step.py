@@ -4,7 +4,10 @@ Linear shape as a graph-captured chain of GEMV launches (us per launch).  With T
 on one box (tools/calls/ab.sh); each line carries a checksum of the step's logits so that identical bits can be
 checked.
 
-    python tools/bench_step.py [reps] [batches, e.g. 1,6] [--step-only]
+    python tools/bench_step.py [reps] [batches, e.g. 1,6] [--step-only] [--copies]
+
+--copies: the batch's rows get B copies of the one window's encoder rows (a B-clip cross-K/V block, as before the
+shared fallback-batch K/V) instead of the shared Tk rows.
 """
 import os
 import sys
@@ -38,13 +41,13 @@ def _chain(fn, n=64, reps=10):
     return sorted(ts)[1]
 
 
-def main(reps=20, batches=(1, 6), step_only=False):
+def main(reps=20, batches=(1, 6), step_only=False, copies=False):
     dev = "cuda"
     torch.manual_seed(0)
     t = torch.zeros(1, dtype=torch.int32, device=dev)
     if not step_only:
         _chains(t)
-    _steps(reps, batches)
+    _steps(reps, batches, copies)
 
 
 def _chains(t):
@@ -73,7 +76,7 @@ def _chains(t):
               f"bits {int(C.view(torch.int16).to(torch.int64).sum())}", flush=True)
 
 
-def _steps(reps, batches):
+def _steps(reps, batches, copies=False):
     from oracle.weights import CONFIGS
     from tw.config import WhisperConfig
     from tw.generation import DecodeSession
@@ -84,7 +87,7 @@ def _steps(reps, batches):
     Tk = cfg.max_source_positions
     for B in batches:
         enc = (torch.randn(Tk, d, device=dev) * 0.5).to(h)
-        sess = DecodeSession(m, enc, B, Tk, 256)
+        sess = DecodeSession(m, enc.repeat(B, 1) if copies and B > 1 else enc, B, Tk, 256)
         sess.t_dev.fill_(100)
         sess.cur.fill_(50364)
         g = torch.cuda.CUDAGraph()
@@ -104,7 +107,7 @@ def _steps(reps, batches):
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) / reps)
-        print(f"step   large-v2 fp16 batch {B} at t=100  {sorted(ts)[1]:7.3f} ms/step  "
+        print(f"step   large-v2 fp16 batch {B}{' (K/V copies)' if copies and B > 1 else ''} at t=100  {sorted(ts)[1]:7.3f} ms/step  "
               f"bits {int(sess.logits.view(torch.int16).to(torch.int64).sum())}", flush=True)
         del sess, g
 
@@ -112,4 +115,4 @@ def _steps(reps, batches):
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     main(int(args[0]) if args else 20, tuple(int(b) for b in args[1].split(",")) if len(args) > 1 else (1, 6),
-         "--step-only" in sys.argv)
+         "--step-only" in sys.argv, "--copies" in sys.argv)

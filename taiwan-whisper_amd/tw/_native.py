@@ -46,6 +46,7 @@ SIGNATURES = {
     "tw_shift_tokens_right": [P, P, I32, I32, I64, I64, P],
     "tw_count_valid": [P, I64, P, P],
     "tw_decode_attn": [P, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, I32, P, I32, F32, I32, P],
+    "tw_decode_attn_hs": [P, I64, P, I64, I64, I64, P, I64, I64, I64, P, I64, I32, I32, I32, P, I32, F32, I32, P],
     "tw_greedy_select": [P, I64, I32, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P],
     "tw_greedy_select_ts": [P, I64, I32, I32, I32, P, P, I64, P, P, I64, I32, P, P, I32, I32, I32, I32, P, P],
     "tw_select_sample": [P, I64, I32, I32, I32, P, P, I32, I64, P, P, I64, I32, P, P, I32, P, P, P],

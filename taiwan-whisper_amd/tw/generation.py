@@ -58,6 +58,8 @@ class DecodeSession:
         else:
             self.cross_kv = [torch.empty(B * Tk, 2 * d, dtype=act, device=dev)
                              for _ in range(cfg.decoder_layers)]
+        self.graph = None
+        self.xkv_shared = False
         self.set_encoder(enc16)
         self.t_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cur = torch.zeros(B, dtype=torch.int64, device=dev)       # this step's input ids
@@ -68,7 +70,6 @@ class DecodeSession:
         self.q = torch.empty(B, d, dtype=act, device=dev)
         self.h = torch.empty(B, cfg.decoder_ffn_dim, dtype=act, device=dev)
         self.logits = torch.empty(B, model.Vp, dtype=act, device=dev)
-        self.graph = None
         # batch <= 8 on the bf16 / fp16 paths: every Linear is one GEMV launch, with the LayerNorm in front of it
         # fused when the residual stream is 16-bit (bit-identical A); larger batches use the skinny GEMM with a
         # separate LayerNorm
@@ -82,6 +83,14 @@ class DecodeSession:
         m, d = self.m, self.d
         shared = enc16.shape[0] == self.Tk and self.B > 1
         nb = 1 if shared else self.B
+        # head-major and shared: ONE clip's K/V blocks ([H][Tk][64] K then V, at the front of each layer's buffer),
+        # read by every row with batch stride 0 (tw_decode_attn_hs) instead of B copies: the fallback batch's
+        # cross-attention reads 1/B of the bytes and each row still sees exactly its batch-1 K/V.  The captured step
+        # bakes the call's strides in, so a change of mode drops the graph (recaptured on the next run)
+        xs = self.hm and shared
+        if self.graph is not None and xs != self.xkv_shared:
+            self.graph = None
+        self.xkv_shared = xs
         # head-major: the projection goes through one [B*Tk][2d] scratch block that lives only for this call
         # (3.9 GB at the 512-clip large-v2 batch; the caching allocator reuses it for the next window)
         proj = torch.empty(nb * self.Tk, 2 * d, dtype=m.act_dtype, device=m.device) if self.hm or shared else None
@@ -89,11 +98,9 @@ class DecodeSession:
             p = f"model.decoder.layers.{i}.encoder_attn"
             wkv = m.wspan(p + ".k_proj.weight", p + ".v_proj.weight", (2 * d, d))
             bkv = m.wspan(p + ".k_proj.zero_bias", p + ".v_proj.bias", (2 * d,))
-            if self.hm and shared:               # K [B][H][Tk][64] then V: one clip's blocks, copied to every row
+            if self.hm and shared:               # K [H][Tk][64] then V of the one clip, shared by every row
                 m._lin(enc16, wkv, bkv, proj)
-                one = torch.empty(2 * self.H * self.Tk * 64, dtype=m.act_dtype, device=m.device)
-                F.kv_head_major(proj, 2 * d, one, 1, self.Tk, self.H)
-                kv.view(2, self.B, -1).copy_(one.view(2, 1, -1).expand(-1, self.B, -1))
+                F.kv_head_major(proj, 2 * d, kv, 1, self.Tk, self.H)
             elif self.hm:
                 m._lin(enc16, wkv, bkv, proj)
                 F.kv_head_major(proj, 2 * d, kv, nb, self.Tk, self.H)
@@ -161,7 +168,11 @@ class DecodeSession:
             self._ln_lin(x, p + ".encoder_attn_layer_norm", m._w16(p + ".encoder_attn.q_proj.weight"),
                          m._w16(p + ".encoder_attn.q_proj.bias"), self.q)
             kv = self.cross_kv[i]
-            if self.hm:         # B*H one-head clips over contiguous [Tk][64] runs
+            if self.xkv_shared:     # every row over the one clip's [H][Tk][64] blocks (batch stride 0)
+                n1 = H * self.Tk * 64
+                F.decode_attn(self.q, d, kv, 64, 0, kv[n1:], 64, 0, o, d, B, H, self.Tk, 0.125, hsk=self.Tk * 64,
+                              hsv=self.Tk * 64)
+            elif self.hm:         # B*H one-head clips over contiguous [Tk][64] runs
                 hv = B * H * self.Tk * 64
                 F.decode_attn(self.q, 64, kv, 64, self.Tk * 64, kv[hv:], 64, self.Tk * 64, o, 64, B * H, 1,
                               self.Tk, 0.125)

@@ -365,25 +365,32 @@ def gelu_bwd(g, pre, out):
 
 
 # ----------------------------------------------------------------------------- greedy decode (A12)
-def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_dev=None, tk_max=None):
+def decode_attn(q, sqb, k, ldk, skb, v, ldv, svb, o, sob, B, H, Tk, scale, tk_dev=None, tk_max=None, hsk=None,
+                hsv=None):
     """One query row per (b, h) over the first Tk (+ *tk_dev) cached key rows (include/tw_hip.h).
-    With tk_dev the host cannot know Tk: tk_max bounds the rows checked for extent."""
+    With tk_dev the host cannot know Tk: tk_max bounds the rows checked for extent.  hsk / hsv: head strides of
+    K / V (tw_decode_attn_hs; default 64, heads side by side in a row); skb = svb = 0 shares one clip's K/V."""
     hd = 64
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
         assert t.dtype == q.dtype and t.dtype in (torch.bfloat16, torch.float16, torch.float32), nm
     rows = Tk if tk_dev is None else tk_max
+    hk, hv = (hd if hsk is None else int(hsk)), (hd if hsv is None else int(hsv))
     _need(q, (B - 1) * sqb + H * hd, "decode q")
-    _need(k, (B - 1) * skb + (rows - 1) * ldk + H * hd, "decode k")
-    _need(v, (B - 1) * svb + (rows - 1) * ldv + H * hd, "decode v")
+    _need(k, (B - 1) * skb + (rows - 1) * ldk + (H - 1) * hk + hd, "decode k")
+    _need(v, (B - 1) * svb + (rows - 1) * ldv + (H - 1) * hv + hd, "decode v")
     _need(o, (B - 1) * sob + H * hd, "decode o")
     if tk_dev is not None:
         assert tk_dev.dtype == torch.int32 and tk_max is not None
     # algorithmic bytes (KernelTimer family "decode_attn_cross" / "decode_attn_self"): every K and V
     # element of the rows attended once (self: the host does not know *tk_dev; tk_max bounds it)
     work = 2 * B * rows * H * hd * q.element_size()
-    KernelTimer.wrap("decode_attn_self" if tk_dev is not None else "decode_attn_cross", work, lambda: call(
-        "tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb, o.data_ptr(), sob,
-        B, H, Tk, _ptr(tk_dev), hd, float(scale), _dt(q), _stream()))
+    if hsk is None and hsv is None:
+        fn = lambda: call("tw_decode_attn", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, v.data_ptr(), ldv, svb,
+                          o.data_ptr(), sob, B, H, Tk, _ptr(tk_dev), hd, float(scale), _dt(q), _stream())
+    else:
+        fn = lambda: call("tw_decode_attn_hs", q.data_ptr(), sqb, k.data_ptr(), ldk, skb, hk, v.data_ptr(), ldv, svb,
+                          hv, o.data_ptr(), sob, B, H, Tk, _ptr(tk_dev), hd, float(scale), _dt(q), _stream())
+    KernelTimer.wrap("decode_attn_self" if tk_dev is not None else "decode_attn_cross", work, fn)
     return o
 
 
