@@ -500,9 +500,14 @@ def gen_lv2_decode(out):
                                    (run_pseudo_labelling.py:917-922 without timestamps)
       {tag}_ts_ids / _margin     : return_timestamps=True, language zh, 48 new tokens, one clip per call (rows
                                    padded with -1; margins [step, clip], nan-padded)
-      f32_long_ids, _long_avg_logprobs, _long_ns_probs, _long_margin, _long_window_steps : 45 s long-form (2 windows),
+      f32_long_ids, _long_avg_logprobs, _long_ns_probs, _long_margin, _long_window_steps, _long_window_ids : 45 s
+                                   long-form (11 windows, each run to max_length),
                                    temperature (0.0,), thresholds that never fire, per-window gates (run_eval.py:659-665)
-    _margin = per step and row, the top-1 minus top-2 processed score (_MarginSpy)."""
+    _margin = per step and row, the top-1 minus top-2 processed score (_MarginSpy).
+    The committed fixture was made as three processes (LV2_TAGS=f32 and f16 at OMP_NUM_THREADS=4, b16 at 8, then
+    `make_golden.py lv2_merge`): CPU bf16 autocast matmuls depend on the thread count, and at 4 threads one b16 greedy
+    row emits a timestamp pair, after which HF's seek loop decodes a second window for that row even without
+    return_timestamps (a path the engine's decoder_input_ids decode does not take)."""
     import contextlib
     from transformers.generation.logits_process import LogitsProcessorList
     from oracle.weights import lv2_decode_weights
@@ -545,12 +550,13 @@ def gen_lv2_decode(out):
             lt = torch.from_numpy(lf).to(dt)
             kw = dict(attention_mask=torch.ones(1, lt.shape[-1], dtype=torch.long), return_timestamps=True,
                       language="zh", task="transcribe")
-            rec = {"avg": [], "ns": [], "steps": []}
+            rec = {"avg": [], "ns": [], "steps": [], "raw": []}
             orig_need = type(m)._need_fallback
 
             def need_spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
                          temperature):
                 rec["steps"].append(len(seek_outputs[index]["scores"]))
+                rec["raw"].append([int(t) for t in seek_sequence.tolist()])
                 rec["avg"].append(float(self._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence,
                                                                     temperature)))
                 from transformers.generation.logits_process import WhisperNoSpeechDetection
@@ -571,6 +577,9 @@ def gen_lv2_decode(out):
             out[f"{tag}_long_avg_logprobs"] = np.array(rec["avg"], dtype=np.float64)
             out[f"{tag}_long_ns_probs"] = np.array(rec["ns"], dtype=np.float64)
             out[f"{tag}_long_window_steps"] = np.array(rec["steps"], dtype=np.int64)
+            # each window's tokens as HF's gate saw them (seek_sequence), -1-padded [window, token]
+            Lw = max(len(r_) for r_ in rec["raw"])
+            out[f"{tag}_long_window_ids"] = np.array([r_ + [-1] * (Lw - len(r_)) for r_ in rec["raw"]], dtype=np.int64)
             # one row per decode step over both windows, in order (batch of one)
             out[f"{tag}_long_margin"] = np.concatenate([s_.reshape(-1) for s_ in spy.steps])
             print(tag, "long-form done", flush=True)
