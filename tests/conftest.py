@@ -33,7 +33,7 @@ def _heartbeat_start():
         while True:
             time.sleep(60)
             tid = _current["id"]
-            if tid is not None:
+            if tid is not None and time.time() - _current["t0"] >= 55:
                 os.write(fd, f"[tests] {tid} running for {time.time() - _current['t0']:.0f} s\n".encode())
     threading.Thread(target=beat, daemon=True).start()
 
