@@ -1088,7 +1088,11 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   p.res = res; p.ldr = ldr; p.res_dtype = res_dtype; p.res_mod = 0;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.c_dtype = c_dtype; p.flags = flags;
   // one output column per wave, or 8 for very wide N (the LM head: fewer workgroups repeating the A prologue)
-  const int cpw = N >= 16384 ? 8 : 1;
+  // one output column per wave; 8 for very wide N (the LM head: fewer workgroups repeating the A prologue), 4 of
+  // them at 5..8 rows (8 x 8 accumulators and their preloads cap a wave at 2 per SIMD); 2 for the wide decode Linears
+  // (fc1, QKV) at 3..8 rows, so each LDS read of the staged rows feeds two columns.  The per-output arithmetic does
+  // not depend on the column count (tests/test_kernels_gpu.py::test_gemv_rows_independent_of_batch)
+  const int cpw = N >= 16384 ? (mr == 8 ? 4 : 8) : (mr >= 4 && N >= 3072 && K <= 1536) ? 2 : 1;
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
   const size_t lds = (size_t)mr * K * 2;
 #define TW_GEMV(MR_, CPW_, PRE_) \
@@ -1096,8 +1100,12 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   if (cpw == 8) {
     if (mr == 1) TW_GEMV(1, 8, 3);
     else if (mr == 2) TW_GEMV(2, 8, 3);
-    else if (mr == 4) TW_GEMV(4, 8, 3);
-    else TW_GEMV(8, 8, 3);
+    else TW_GEMV(4, 8, 3);
+  } else if (cpw == 4) {
+    TW_GEMV(8, 4, 3);
+  } else if (cpw == 2) {
+    if (mr == 4) TW_GEMV(4, 2, 3);
+    else TW_GEMV(8, 2, 3);
   } else if (K <= 1536) {
     if (mr == 1) TW_GEMV(1, 1, 3);
     else if (mr == 2) TW_GEMV(2, 1, 3);

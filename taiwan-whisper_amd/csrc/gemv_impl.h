@@ -85,6 +85,38 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
       for (int c = 0; c < 5; ++c) t[j][c] = c < nch ? *(const bf16x8*)(xr + (c * 32 + hl) * 8) : bf16x8{};
     }
+    // the statistics of the wave's rows in lockstep: their butterflies interleave instead of running one after the
+    // other (each row's own sums keep the order below, so A stays bit-identical)
+    float s[RPW], mean[RPW], rstd[RPW];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      s[j] = 0.f;
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+        if (c < nch)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) s[j] += e2f<H>(t[j][c][q]);
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) s[j] += __shfl_xor(s[j], o, 64);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      mean[j] = s[j] / K;
+      s[j] = 0.f;
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+        if (c < nch)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[j][c][q]) - mean[j]; s[j] += d * d; }
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) s[j] += __shfl_xor(s[j], o, 64);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) rstd[j] = rsqrtf(s[j] / K + eps);
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int row = wave + j * nw;
@@ -94,24 +126,6 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
         for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = bf16x8{};
         continue;
       }
-      float s = 0.f;
-#pragma unroll
-      for (int c = 0; c < 5; ++c)
-        if (c < nch)
-#pragma unroll
-          for (int q = 0; q < 8; ++q) s += e2f<H>(t[j][c][q]);
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      const float mean = s / K;
-      float ss = 0.f;
-#pragma unroll
-      for (int c = 0; c < 5; ++c)
-        if (c < nch)
-#pragma unroll
-          for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[j][c][q]) - mean; ss += d * d; }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-      const float rstd = rsqrtf(ss / K + eps);
       if (lane < 32) {
 #pragma unroll
         for (int c = 0; c < 5; ++c) {
@@ -124,8 +138,8 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
             bf16x8 o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              o[q] = f2e<H>((e2f<H>(t[j][c][q]) - mean) * rstd * w0[q] + b0[q]);
-              o[q + 4] = f2e<H>((e2f<H>(t[j][c][q + 4]) - mean) * rstd * w1[q] + b1[q]);
+              o[q] = f2e<H>((e2f<H>(t[j][c][q]) - mean[j]) * rstd[j] * w0[q] + b0[q]);
+              o[q + 4] = f2e<H>((e2f<H>(t[j][c][q + 4]) - mean[j]) * rstd[j] * w1[q] + b1[q]);
             }
             *(bf16x8*)(dst + (c * 32 + hl) * 8) = o;
           }

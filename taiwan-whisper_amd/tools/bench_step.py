@@ -4,7 +4,7 @@ Linear shape as a graph-captured chain of GEMV launches (us per launch).  With T
 on one box (tools/calls/ab.sh); each line carries a checksum of the step's logits so that identical bits can be
 checked.
 
-    python tools/bench_step.py [reps] [batches, e.g. 1,6] [--step-only] [--copies]
+    python tools/bench_step.py [reps] [batches, e.g. 1,6] [--step-only] [--copies] [--rows=N]
 
 --copies: the batch's rows get B copies of the one window's encoder rows (a B-clip cross-K/V block, as before the
 shared fallback-batch K/V) instead of the shared Tk rows.
@@ -41,22 +41,22 @@ def _chain(fn, n=64, reps=10):
     return sorted(ts)[1]
 
 
-def main(reps=20, batches=(1, 6), step_only=False, copies=False):
+def main(reps=20, batches=(1, 6), step_only=False, copies=False, rows=1):
     dev = "cuda"
     torch.manual_seed(0)
     t = torch.zeros(1, dtype=torch.int32, device=dev)
     if not step_only:
-        _chains(t)
+        _chains(t, rows)
     _steps(reps, batches, copies)
 
 
-def _chains(t):
+def _chains(t, rows=1):
     dev = "cuda"
     print(f"floor  step_advance chain {_chain(lambda: F.step_advance(t)):7.2f} us/launch", flush=True)
     h = torch.float16
     d, ffn = 1280, 5120
-    x = (torch.randn(1, d, device=dev) * 0.5).to(h)
-    xf = (torch.randn(1, ffn, device=dev) * 0.5).to(h)
+    x = (torch.randn(rows, d, device=dev) * 0.5).to(h)
+    xf = (torch.randn(rows, ffn, device=dev) * 0.5).to(h)
     lnw, lnb = torch.rand(d, device=dev) + 0.5, torch.randn(d, device=dev) * 0.1
     for name, N, K, ln, res, fl in (("d x d  (out_proj, +res)", d, d, False, True, F.GEMM_ROUND),
                                     ("d x d  (LN + cross q)", d, d, True, False, F.GEMM_ROUND),
@@ -65,14 +65,14 @@ def _chains(t):
                                     ("d x 4d (fc2, +res)", d, ffn, False, True, F.GEMM_ROUND)):
         W = (torch.randn(N, K, device=dev) * 0.02).to(h)
         b = (torch.randn(N, device=dev) * 0.1).to(h)
-        C = torch.empty(1, N, dtype=h, device=dev)
-        r = torch.randn(1, N, device=dev).to(h) if res else None
+        C = torch.empty(rows, N, dtype=h, device=dev)
+        r = torch.randn(rows, N, device=dev).to(h) if res else None
         a = xf if K == ffn else x
         kw = dict(bias=b, res=r, flags=fl)
         if ln:
             kw.update(ln_w=lnw, ln_b=lnb)
         us = _chain(lambda: F.gemv(a, W, C, **kw))
-        print(f"gemv   {name:24s} {us:7.2f} us/launch  {N * K * 2 / us / 1e3:7.1f} GB/s  "
+        print(f"gemv   {name:24s} x{rows} {us:7.2f} us/launch  {N * K * 2 / us / 1e3:7.1f} GB/s  "
               f"bits {int(C.view(torch.int16).to(torch.int64).sum())}", flush=True)
 
 
@@ -115,4 +115,5 @@ def _steps(reps, batches, copies=False):
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     main(int(args[0]) if args else 20, tuple(int(b) for b in args[1].split(",")) if len(args) > 1 else (1, 6),
-         "--step-only" in sys.argv, "--copies" in sys.argv)
+         "--step-only" in sys.argv, "--copies" in sys.argv,
+         int(next((a.split("=")[1] for a in sys.argv if a.startswith("--rows=")), 1)))
