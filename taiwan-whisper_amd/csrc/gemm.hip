@@ -572,9 +572,21 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemmP p, const float* __restr
   bf16* xs = (bf16*)gemv_smem;                         // [MR][K] bf16
   const int lane = lane_id(), wave = wave_id_uniform();
   const int n0 = (blockIdx.x * 4 + wave) * CPW;
+  // LayerNorm'd rows (K <= 1280, K % 256 == 0): the LN weight and bias go to LDS behind the rows ([2][K] fp32) by
+  // LDS-DMA issued first, so they travel with the weight preload and the row loads instead of after the statistics
+  float* lnp = nullptr;
+  if (lnw && p.K <= 1280) {
+    lnp = (float*)(gemv_smem + (size_t)MR * p.K * 2);
+    const int per = p.K / 256;                         // 64-lane x 16-B pieces per array
+    for (int i = wave; i < 2 * per; i += 4) {
+      const float* src = i < per ? lnw : lnb;
+      const int pc = (i % per) * 64;
+      buf_load_lds16(make_rsrc(src), lnp + (i < per ? 0 : p.K) + pc * 4, (uint32_t)(pc + lane) * 16);
+    }
+  }
   bf16x8 wpre[CPW][PRE];
   gemv_preload<H, CPW, PRE>(p, n0, lane, wpre);
-  gemv_stage_rows<H, MR>(p, lnw, lnb, eps, xs, wave, 4, lane);
+  gemv_stage_rows<H, MR>(p, lnw, lnb, eps, xs, wave, 4, lane, lnp);
   __syncthreads();
   if (n0 >= p.N) return;
   gemv_finish<H, MR, CPW, PRE>(p, kv, xs, n0, lane, wpre);
@@ -1094,7 +1106,7 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   // not depend on the column count (tests/test_kernels_gpu.py::test_gemv_rows_independent_of_batch)
   const int cpw = N >= 16384 ? (mr == 8 ? 4 : 8) : (mr >= 4 && N >= 3072 && K <= 1536) ? 2 : 1;
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
-  const size_t lds = (size_t)mr * K * 2;
+  const size_t lds = (size_t)mr * K * 2 + (ln_w && K <= 1280 ? (size_t)2 * K * 4 : 0);
 #define TW_GEMV(MR_, CPW_, PRE_) \
   hipLaunchKernelGGL((gemv_kernel<H, MR_, CPW_, PRE_>), grid, dim3(256), lds, stream, p, ln_w, ln_b, eps, kv)
   if (cpw == 8) {

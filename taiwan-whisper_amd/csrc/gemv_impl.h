@@ -69,12 +69,12 @@ __device__ __forceinline__ void gemv_preload(const GemmP& p, int n0, int lane, b
 template <bool H, int MR>
 __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __restrict__ lnw,
                                                 const float* __restrict__ lnb, float eps, bf16* xs, int wave, int nw,
-                                                int lane) {
+                                                int lane, const float* lnp = nullptr) {
   const int K = p.K;
-  if (MR > 1 && lnw && K <= 1280) {
-    // batches of 2..8 rows: one global pass -- every row of this wave (rows wave, wave + nw, ...) loaded to
-    // registers at once, then the same half-wave statistics in the same order as below
-    // (bit-identical A).  At MR = 1 the three-pass form measured faster (profiles/r05_j_gemv_variants_ab.log)
+  if (lnp) {
+    // one global pass: every row of this wave (rows wave, wave + nw, ...) loaded to registers at once while the LN
+    // parameters arrive in LDS (lnp: w then b, the kernel's LDS-DMA at entry), then the same half-wave statistics
+    // in the same order as below (bit-identical A); one round trip to memory instead of two or three
     constexpr int RPW = (MR + 3) / 4;
     const int hl = lane & 31, nch = K / 256;
     bf16x8 t[RPW][5];
@@ -117,6 +117,8 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
       for (int j = 0; j < RPW; ++j) s[j] += __shfl_xor(s[j], o, 64);
 #pragma unroll
     for (int j = 0; j < RPW; ++j) rstd[j] = rsqrtf(s[j] / K + eps);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of the LN parameters have landed
+    __syncthreads();                                    // ... and every other wave's
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int row = wave + j * nw;
@@ -130,11 +132,11 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
         for (int c = 0; c < 5; ++c) {
           if (c < nch) {
-            // LN parameters loaded here, not with the rows: held for every chunk they cost ~80 VGPRs, which at
-            // MR = 8 cut the waves per SIMD below what the wide Linears (fc1: 5 waves per SIMD) need
+            // LN parameters from LDS, read per chunk (held for every chunk they would cost ~80 VGPRs: at MR = 8 that
+            // cut the waves per SIMD below what the wide Linears need)
             const int e = (c * 32 + hl) * 8;
-            const f32x4 w0 = *(const f32x4*)(lnw + e), w1 = *(const f32x4*)(lnw + e + 4);
-            const f32x4 b0 = *(const f32x4*)(lnb + e), b1 = *(const f32x4*)(lnb + e + 4);
+            const f32x4 w0 = *(const f32x4*)(lnp + e), w1 = *(const f32x4*)(lnp + e + 4);
+            const f32x4 b0 = *(const f32x4*)(lnp + K + e), b1 = *(const f32x4*)(lnp + K + e + 4);
             bf16x8 o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
