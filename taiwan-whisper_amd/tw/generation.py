@@ -340,7 +340,7 @@ class _Decoder:
 
 
 class _BeamDecoder:
-    """Beam search over B clips x k beams with the same prompt (short-form, no timestamps): HF
+    """Beam search over B clips x k beams with the same prompt (with `timestamps`, one window of the seek loop): HF
     GenerationMixin._beam_search (transformers 5.15 generation/utils.py:3208-3560), the search behind
     `training/run_eval.py:144-147` (--num_beams) and `run_distillation.py:1476-1484` (generation_num_beams).
     The B*k rows decode as one batch on the engine's step (DecodeSession, every clip's encoder rows repeated k
