@@ -63,6 +63,28 @@ def test_decode_attn(B, H, Tk, dev):
     assert err.max() <= 2 ** -7 * ref.abs().max() + 1e-3
 
 
+@pytest.mark.parametrize("B,H,Tk,dt", [(6, 20, 1500, torch.float16), (5, 2, 1500, torch.bfloat16), (3, 4, 37, torch.float32),
+                                       (40, 20, 1500, torch.float16)])
+def test_decode_attn_head_strides_shared_kv(B, H, Tk, dt):
+    """tw_decode_attn_hs: one clip's head-major K/V ([H][Tk][64] K then V) read by every row of a batch with batch
+    stride 0 (the temperature-fallback batch, tw.generation.DecodeSession.set_encoder) == the same rows over B
+    copies through tw_decode_attn (B*H one-head clips), bit for bit, on the split (< 640 pairs) and the
+    one-workgroup-per-pair kernels."""
+    from tw import ops
+    g = torch.Generator().manual_seed(B * 7 + Tk)
+    q = (torch.randn(B, H * 64, generator=g)).to(dt).to(DEV)
+    one = (torch.randn(2 * H * Tk * 64, generator=g)).to(dt).to(DEV)        # K [H][Tk][64] then V
+    n1 = H * Tk * 64
+    o1 = torch.empty(B, H * 64, dtype=dt, device=DEV)
+    ops.decode_attn(q, H * 64, one, 64, 0, one[n1:], 64, 0, o1, H * 64, B, H, Tk, 0.125, hsk=Tk * 64, hsv=Tk * 64)
+    # B copies in the B*H one-head-clip form the non-shared head-major path uses
+    rep = torch.cat([one[:n1].repeat(B), one[n1:].repeat(B)])
+    hv = B * n1
+    o2 = torch.empty(B, H * 64, dtype=dt, device=DEV)
+    ops.decode_attn(q, 64, rep, 64, Tk * 64, rep[hv:], 64, Tk * 64, o2, 64, B * H, 1, Tk, 0.125)
+    assert torch.equal(o1, o2)
+
+
 @pytest.mark.parametrize("B,Tk,H,dt", [(3, 1500, 20, torch.bfloat16), (2, 7, 2, torch.float32), (1, 1500, 6, torch.bfloat16)])
 def test_kv_head_major(B, Tk, H, dt):
     """tw_kv_head_major is the exact permutation [B*Tk][k | v] -> K [B][H][Tk][64], V [B][H][Tk][64] (a padded
