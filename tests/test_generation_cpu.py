@@ -100,3 +100,43 @@ def test_fallback_batch_only_where_rows_are_independent(monkeypatch, compute, ba
     generation._longform(m, gc, feats, None, "zh", "transcribe", None, 40, False, 3000, trace,
                          temperature=(0.0, 0.2, 0.4, 0.6), compression_ratio_threshold=1.35, fallback_batch=True)
     assert any(t["batch"] > 1 for t in trace) == batched
+
+
+@pytest.mark.parametrize("ngen", [0, 1, 2, 5])
+def test_beam_timestamp_rules_match_oracle(ngen):
+    """The beam decoder's vectorised HF WhisperTimeStampLogitsProcessor (generation._BeamDecoder._ts_rules, applied
+    to the B*k processed log-prob rows) masks exactly what the per-row oracle restatement (oracle/greedy_ref.py
+    timestamp_rules) masks, for histories with text, single and paired timestamps, at the first step and later;
+    some rows carry enough timestamp mass to trigger the "timestamps beat every text token" rule."""
+    from oracle.greedy_ref import timestamp_rules
+    V, tb, no_ts, eos, P, mi = 51865, 50364, 50363, 50257, 3, 50
+    B, nb = 3, 4
+    g = torch.Generator().manual_seed(17 + ngen)
+    run_seq = torch.full((B, nb, P + 12), 50257, dtype=torch.int64)
+    run_seq[:, :, :P] = torch.tensor([50258, 50260, 50359])
+    last_ts = torch.full((B, nb), -1, dtype=torch.int64)
+    gens = []
+    for r in range(B * nb):
+        gen, t_last = [], tb
+        for i in range(ngen):
+            kind = int(torch.randint(0, 3, (1,), generator=g))
+            if kind == 0 or (i > 0 and gen[-1] >= tb and (i < 2 or gen[-2] >= tb)):
+                tok = int(torch.randint(0, eos, (1,), generator=g))          # text
+            else:
+                t_last = t_last + int(torch.randint(0, 30, (1,), generator=g))
+                tok = t_last                                                    # a non-decreasing timestamp
+            gen.append(tok)
+        gens.append(gen)
+        run_seq[r // nb, r % nb, P:P + ngen] = torch.tensor(gen, dtype=torch.int64)
+        stamps = [t for t in gen if t >= tb]
+        last_ts[r // nb, r % nb] = stamps[-1] if stamps else -1
+    logits = torch.randn(B * nb, V, generator=g) * 3
+    logits[::3, tb:] += 6.0                                                     # timestamp-heavy rows
+    logp = torch.log_softmax(logits, -1)
+    ns = types.SimpleNamespace(ts=(tb, no_ts, mi), eos=eos, P=P)
+    got = generation._BeamDecoder._ts_rules(ns, logp.clone(), run_seq, last_ts, P + ngen)
+    for r in range(B * nb):
+        want = timestamp_rules(logp[r], gens[r], ngen == 0, ts_begin=tb, no_ts=no_ts, eos=eos, max_initial=mi)
+        assert torch.equal(torch.isinf(got[r]), torch.isinf(want)), (r, gens[r])
+        fin = ~torch.isinf(want)
+        assert torch.equal(got[r][fin], want[fin]), r
