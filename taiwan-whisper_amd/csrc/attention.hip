@@ -280,9 +280,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
   // epilogue
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
-    float lt = l[qi];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = swap32_sum(swap16_sum(l[qi]));   // xor 16 then 32 on permlane swaps (bit-identical: common.h)
     const int q = qw + qi * 16 + li;
     if (q < p.Tq) {
       const float inv = 1.f / lt;
@@ -308,7 +306,7 @@ __global__ void attn_bwd_pre_kernel(const bf16* __restrict__ dO, int64_t lddo, c
   const int h = w % H;
   const int64_t row = w / H;   // b*Tq + q
   const float v = bf2f(dO[row * lddo + h * 64 + lane]) * bf2f(O[row * ldo + h * 64 + lane]);
-  const float s = wave_sum(v);
+  const float s = wave_sum_dpp(v);
   if (lane == 0) {
     const int b = row / Tq, q = row % Tq;
     Dv[((int64_t)b * H + h) * Tq + q] = s;
