@@ -1104,7 +1104,7 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   // them at 5..8 rows (8 x 8 accumulators and their preloads cap a wave at 2 per SIMD); 2 for the wide decode Linears
   // (fc1, QKV) at 3..8 rows, so each LDS read of the staged rows feeds two columns.  The per-output arithmetic does
   // not depend on the column count (tests/test_kernels_gpu.py::test_gemv_rows_independent_of_batch)
-  const int cpw = N >= 16384 ? (mr == 8 ? 4 : 8) : (mr >= 4 && N >= 3072 && K <= 1536) ? 2 : 1;
+  const int cpw = N >= 16384 ? (mr == 8 || mr == 1 ? 4 : 8) : (mr >= 4 && N >= 3072 && K <= 1536) ? 2 : 1;
   const dim3 grid((N + 4 * cpw - 1) / (4 * cpw));
   const size_t lds = (size_t)mr * K * 2 + (ln_w && K <= 1280 ? (size_t)2 * K * 4 : 0);
 #define TW_GEMV(MR_, CPW_, PRE_) \
@@ -1114,7 +1114,8 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
     else if (mr == 2) TW_GEMV(2, 8, 3);
     else TW_GEMV(4, 8, 3);
   } else if (cpw == 4) {
-    TW_GEMV(8, 4, 3);
+    if (mr == 1) TW_GEMV(1, 4, 3);
+    else TW_GEMV(8, 4, 3);
   } else if (cpw == 2) {
     if (mr == 4) TW_GEMV(4, 2, 3);
     else TW_GEMV(8, 2, 3);
