@@ -101,9 +101,11 @@ def cpu_baseline(seconds_budget=20.0):
     from oracle.weights import CONFIGS, make_weights
     from oracle.whisper_ref import Ref, to_torch
     # the job's CPU share: OMP_NUM_THREADS where the launcher sets it (the GPU box gives a 1-GPU job 16 threads of a
-    # much larger host), else every CPU this process may run on
+    # much larger host; only the first field of a nested value such as "16,1" counts), else the CPUs this process may
+    # run on, capped at 16 so that `cores` stays comparable across hosts and rounds
     host = os.cpu_count() or 1
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0)) or host
+    omp = (os.environ.get("OMP_NUM_THREADS") or "").split(",")[0].strip()
+    threads = int(omp) if omp.isdigit() and int(omp) > 0 else min(16, len(os.sched_getaffinity(0)) or host)
     torch.set_num_threads(threads)
     cfg = CONFIGS["tiny"]
     ps = to_torch(make_weights(cfg, 1))
@@ -139,14 +141,25 @@ def cpu_baseline(seconds_budget=20.0):
                        f"AdamW) via oracle/distill_ref.py, {len(steady)} steady steps of {len(times)}")
 
 
-def load_pmc(kernel_family):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary."""
-    p = os.path.join(REPO, "profiles", "pmc_latest.json")
+PMC_FILE = "profiles/pmc_latest.json"
+MFMA_FILE = "profiles/mfma_latest.json"
+
+
+def _committed(path):
+    """(summary dict, source note) of a committed rocprofv3 --pmc summary: the file's own `source` field names the
+    command, tree and box it came from (PMC counters need their own profiler passes, so they are never this run's)."""
+    p = os.path.join(REPO, path)
     if not os.path.exists(p):
-        return None
+        return {}, None
     with open(p) as f:
         d = json.load(f)
-    return d.get(kernel_family, {}).get("hbm_bytes_per_launch")
+    return d, f"{path}: {d.get('source', 'source not recorded')}"
+
+
+def load_pmc(kernel_family):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary, and its source."""
+    d, src = _committed(PMC_FILE)
+    return d.get(kernel_family, {}).get("hbm_bytes_per_launch"), src
 
 
 def decode_bytes_per_step(cfg, B, t_avg, Tk=1500, elem=2):
@@ -213,16 +226,18 @@ def run_decode(args, device, rank, world, pg):
             return m.generate(mel, **kw)
         units_per_step, unit = args.batch, "utt/s"
     else:
+        # --batch N: N recordings in ONE generate call, kept together window after window (HF's batched long-form,
+        # run_eval.py:667-681 with inner_batch_size recordings)
         n = int(args.seconds * 16000)
-        wav = synthetic_audio(1, seed=1000 * rank, seconds=args.seconds, device=device, length=None)
+        wav = synthetic_audio(args.batch, seed=1000 * rank, seconds=args.seconds, device=device, length=None)
         mel_long, _ = fe.extract(wav, want_conv_input=False)           # features prepared outside the timed
-        mask = torch.ones(1, n // 160, dtype=torch.int32, device=device)   # region, as run_eval.py:567-589
+        mask = torch.ones(args.batch, n // 160, dtype=torch.int32, device=device)   # region, as run_eval.py:567-589
         trace = []
 
         def step(i):
             trace.clear()
             return m.generate(mel_long, attention_mask=mask, return_timestamps=True, _trace=trace, **kw)
-        units_per_step, unit = args.seconds, "audio s/s"
+        units_per_step, unit = args.seconds * args.batch, "audio s/s"
     for i in range(args.warmup):
         if c4:
             step(i)
@@ -249,6 +264,7 @@ def run_decode(args, device, rank, world, pg):
         dec_steps = args.steps * (out.shape[1] + 3)                 # prompt prefill (3) + generated columns
         B, t_avg = args.batch, 4 + out.shape[1] / 2
     else:
+        # row-steps (one decoder step of one row); with --batch N the rows of a batch share each launch
         dec_steps = args.steps * sum(len(t["raw"]) + len(t["prompt"]) - 1 for t in trace_last)
         B, t_avg = 1, 4 + sum(len(t["raw"]) for t in trace_last) / max(1, 2 * len(trace_last))
     ms_dec = elapsed / dec_steps * 1e3
@@ -285,12 +301,15 @@ def run_decode(args, device, rank, world, pg):
                 "; eos suppressed -> fixed tokens per clip" if c4 else ""),
             "config": {"workload": (f"c4: whisper-large-v2 batched greedy, {args.batch} x 30 s clips per step, "
                                     f"{args.new_tokens} new tokens" if c4 else
-                                    f"c5: whisper-large-v2 long-form, {args.seconds:.0f} s recording, timestamps, "
-                                    f"max_length 256 per window, long-form kwargs {args.longform_kwargs}"),
+                                    f"c5: whisper-large-v2 long-form, {args.batch} x {args.seconds:.0f} s recording(s) "
+                                    f"in one generate call, timestamps, max_length 256 per window, long-form kwargs "
+                                    f"{args.longform_kwargs}"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch, "parallelism":
                        f"replicas{world}"},
             "decode_steps": dec_steps, "ms_per_decode_step": round(ms_dec, 4),
-            "decode_step_hbm_frac": round(step_bytes / (ms_dec * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            # batch-1 steps only: a row-step of a batched decode shares its weight reads with the batch's other rows
+            "decode_step_hbm_frac": (round(step_bytes / (ms_dec * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+                                     if c4 or args.batch == 1 else None),
             "roofline": roof,
             "cpu_baseline": None,
         }
@@ -361,11 +380,7 @@ def exchange_summary(ev, log, steps, t_rank, pg, world, device):
 def load_mfma(workload, family):
     """MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)) of a kernel family
     from the committed rocprofv3 --pmc summary (tools/pmc_mfma.sh -> profiles/mfma_latest.json)."""
-    p = os.path.join(REPO, "profiles", "mfma_latest.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        d = json.load(f)
+    d, _ = _committed(MFMA_FILE)
     return d.get(workload, {}).get(family, {}).get("mfma_busy_frac")
 
 
@@ -426,12 +441,18 @@ def main():
     # TW_BENCH_REHEARSE=1: all ranks on cuda:0 over gloo (multi-rank rehearsal on a 1-GPU box);
     # the real multi-GPU run uses one GPU per rank and RCCL ("nccl").
     rehearse = os.environ.get("TW_BENCH_REHEARSE") == "1"
+    # TW_BENCH_FORCE_EXCHANGE=1 (rehearsal of the 8-GPU path on one GPU): a process group even at world 1 and the
+    # trainer's DP exchange forced on (per-layer RCCL all-reduces, tail, waits, deferred update), so the line's
+    # `distributed` object comes from the backend the 8-GPU node runs
+    force_x = os.environ.get("TW_BENCH_FORCE_EXCHANGE") == "1"
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    if force_x and env_world is None:         # not under a launcher: a one-rank rendezvous of our own
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+    if world > 1 or force_x:
         if rehearse:
             torch.distributed.init_process_group("gloo")
         else:
@@ -448,7 +469,7 @@ def main():
 
     student, teacher, freeze_encoder = make_models(args, device)
     trainer = DistillationTrainer(student, teacher, learning_rate=1e-4, warmup_steps=0,
-                                  freeze_encoder=freeze_encoder, process_group=pg)
+                                  freeze_encoder=freeze_encoder, process_group=pg, force_exchange=force_x)
     trainer.exchange_events = [] if pg is not None else None     # exposed gradient-exchange waits
     trainer.exchange_log = [] if pg is not None else None        # (bytes, tail) per all-reduced bucket
     fe = WhisperFeatureExtractor(device=device)
@@ -513,7 +534,7 @@ def main():
         roof = None
         if ks is not None:
             achieved = ks["rate"] / 1e12
-            pmc = load_pmc("gemm_nn") if args.config == "c3" else None     # the PMC summary is of c3
+            pmc, pmc_src = load_pmc("gemm_nn") if args.config == "c3" else (None, None)   # the PMC summary is of c3
             roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=pmc,
                         mfma_busy_frac=(load_mfma("c3_step", "gemm_pp (persistent 256x256 forward GEMM)")
@@ -525,7 +546,10 @@ def main():
                         launches_per_step=ks["launches"] // args.steps, avg_launch_ms=round(ks["avg_ms"], 4),
                         algo_tflop_per_launch=round(ks["avg_work"] / 1e12, 4),
                         algo_bytes_per_launch=round(ks["avg_bytes"]),
-                        traffic_over_algo=(round(pmc / ks["avg_bytes"], 3) if pmc and ks["avg_bytes"] else None))
+                        traffic_over_algo=(round(pmc / ks["avg_bytes"], 3) if pmc and ks["avg_bytes"] else None),
+                        # read from committed files, not measured in this run (see each file's `source`)
+                        traffic_source=pmc_src,
+                        mfma_busy_source=_committed(MFMA_FILE)[1] if args.config == "c3" else None)
         out = {
             "metric": "distillation utterances/sec (30 s clips)",
             "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
@@ -543,6 +567,7 @@ def main():
             # share of SIMD-cycles from the committed PMC pass (profiles/mfma_latest.json)
             "teacher_fwd_mfma_frac": None if teacher_ms is None else round(3.445 / teacher_ms / PEAK_BF16_TFLOPS * 1e3, 4),
             "teacher_fwd_mfma_busy_frac": load_mfma("teacher_forward", "ALL_BUT_OTHER"),
+            "teacher_fwd_mfma_busy_source": _committed(MFMA_FILE)[1],
             "model_tflops_per_step_per_gpu": round(flops_clip * args.batch / 1e12, 2),
             "step_mfma_frac": round(flops_clip * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(loss, 4),

@@ -145,34 +145,3 @@ def make_weights(cfg: dict, seed: int, lin_std: float = 0.02, per_tensor: bool =
         return k, _scale(k, z, lin_std, embed_std)
     with ThreadPoolExecutor(max_workers=min(16, len(keys))) as ex:
         return dict(ex.map(one, range(len(keys))))
-
-
-# Decode-parity recipe at real widths (tests/golden/make_golden.py gen_lv2_decode, round 5).  make_weights' default
-# scales give a decoder whose argmax barely depends on the audio at d = 1280 (round 4's fixture produced 2-3 distinct
-# tokens per 48-step row, the same for every clip).  This recipe strengthens the paths that carry the audio and the
-# position into the logits, and the logit scale (fewer near-ties), measured on HF generate at large-v2 dims: 16-20
-# distinct tokens per 48-step greedy row, a different sequence per clip.  (A first round-5 recipe with a peakier
-# cross-attention -- q / k x 10, v / out x 20 -- reached 20-28 distinct tokens but was chaotic: HF's own fp16 and fp32
-# runs parted at the first token.)  Multipliers applied to the float32
-# make_weights(cfg, seed, per_tensor=True, embed_std=0.6) tensors:
-LV2_DECODE_SCALES = {
-    "encoder_attn.q_proj.weight": 7.0,      # std 0.14: cross-attention concentrates on some frames (input-dependent)
-    "encoder_attn.k_proj.weight": 7.0,
-    "encoder_attn.v_proj.weight": 14.0,     # std 0.28: the attended frames carry into the residual stream
-    "encoder_attn.out_proj.weight": 14.0,
-    "decoder.embed_positions.weight": 25.0,  # std 0.5: each step queries different frames
-    "fc1.weight": 2.0,                      # decoder MLP std 0.04
-    "fc2.weight": 2.0,
-}
-
-
-def lv2_decode_weights(cfg: dict, seed: int) -> dict:
-    """make_weights(cfg, seed, per_tensor=True, embed_std=0.6) with LV2_DECODE_SCALES applied to the decoder keys."""
-    w = make_weights(cfg, seed, per_tensor=True, embed_std=0.6)
-    for k in w:
-        if not k.startswith("model.decoder"):
-            continue
-        for pat, s in LV2_DECODE_SCALES.items():
-            if k.endswith(pat):
-                w[k] = (w[k] * np.float32(s)).astype(np.float32)
-    return w

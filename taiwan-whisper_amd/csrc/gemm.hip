@@ -1099,7 +1099,6 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
   p.alpha = 1.f; p.bias = (const bf16*)bias;
   p.res = res; p.ldr = ldr; p.res_dtype = res_dtype; p.res_mod = 0;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.c_dtype = c_dtype; p.flags = flags;
-  // one output column per wave, or 8 for very wide N (the LM head: fewer workgroups repeating the A prologue)
   // one output column per wave; 8 for very wide N (the LM head: fewer workgroups repeating the A prologue), 4 of
   // them at 5..8 rows (8 x 8 accumulators and their preloads cap a wave at 2 per SIMD); 2 for the wide decode Linears
   // (fc1, QKV) at 3..8 rows, so each LDS read of the staged rows feeds two columns.  The per-output arithmetic does

@@ -79,7 +79,7 @@ class DistillationTrainer:
                  lr_scheduler_type: str = "constant_with_warmup", max_steps: int = 0,
                  gradient_accumulation_steps: int = 1, freeze_encoder: bool = True, freeze_decoder: bool = False,
                  freeze_embed_positions: bool = True, process_group=None, dp_bucket_mb: int = 64,
-                 overlap_update: Optional[bool] = None):
+                 overlap_update: Optional[bool] = None, force_exchange: bool = False):
         if student.compute != teacher.compute:
             raise ValueError(f"student computes in {student.compute}, teacher in {teacher.compute}: the reference "
                              "runs both under one mixed_precision setting")
@@ -91,6 +91,11 @@ class DistillationTrainer:
         self.accum = gradient_accumulation_steps
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        # force_exchange (tests, bench rehearsal): run the whole DP exchange -- per-layer async all-reduces from the
+        # backward hook, the tail, the waits, the deferred update -- even on a process group of ONE rank, so the
+        # RCCL code path executes on a 1-GPU box (an all-reduce over one rank is the identity: bit-identical)
+        self.force_exchange = bool(force_exchange) and process_group is not None
+        self.dp = self.world > 1 or self.force_exchange
         self.bucket = dp_bucket_mb * (1 << 20) // 4
         # DDP mean (torch Reducer, no comm hook): every rank's gradient is multiplied by fp32(1/world) as it
         # enters its bucket, then the buckets are SUM-all-reduced.  For a power-of-two world the factor is
@@ -103,7 +108,7 @@ class DistillationTrainer:
         # 265 MB at c3, final only after the embedding backward) then runs beside that encoder instead of
         # stalling the stream.  Same kernels on the same data in the same order per buffer: bit-identical.
         # Any reader of the weights or optimizer state (eval, state dicts, save) calls flush() first.
-        self.overlap_update = (self.world > 1 and freeze_encoder) if overlap_update is None else bool(overlap_update)
+        self.overlap_update = (self.dp and freeze_encoder) if overlap_update is None else bool(overlap_update)
         if self.overlap_update and not freeze_encoder:
             raise ValueError("overlap_update needs a frozen encoder: the next forward must read no trainable weight")
         self._update = None      # (lr, t) of a launched, not yet applied update
@@ -183,7 +188,7 @@ class DistillationTrainer:
         # the backward has finished it (RCCL on its own stream, beside the remaining backward)
         self._pending, self._reduced = [], []
         sync = self.micro + 1 == self.accum or end_of_dataloader
-        self.bw.on_ready = self._grad_ready if (self.world > 1 and sync) else None
+        self.bw.on_ready = self._grad_ready if (self.dp and sync) else None
         Tk = enc16.shape[0] // B
         tape = []
         hs = s.decode(ids, enc16, Tk, tape=tape)
@@ -250,7 +255,7 @@ class DistillationTrainer:
         the backward (per finished layer) are skipped; the rest (embeddings, final LayerNorm, ...) is
         launched now.  Bucketed async SUM all-reduce of the flat fp32 gradient over RCCL, each rank's
         gradient scaled by 1/world first (folded into the loss gradient for power-of-two worlds)."""
-        if self.world == 1:
+        if not self.dp:
             return
         done = sorted(getattr(self, "_reduced", []))
         pos = 0

@@ -673,6 +673,141 @@ def need_fallback(tokens, avg_logprob, no_speech_prob, vocab_size, compression_r
     return needs, skip
 
 
+def _bucket(n):
+    """Decode-batch size for n rows: the next power of two (the extra rows repeat the first one and are dropped), so
+    that a shrinking batch -- recordings finishing, fewer rows falling back -- reuses a captured step."""
+    b = 1
+    while b < n:
+        b *= 2
+    return b
+
+
+def _longform_batched(model, gc, feats, lens, init, temps, track, window, trace, max_length, max_new_tokens,
+                      compression_ratio_threshold, logprob_threshold, no_speech_threshold, fallback_batch, decoder, trim,
+                      seeds_of, ns_token, ts_begin, eos, pad, enc_rows=32):
+    """HF's batched sequential long-form (generation_whisper.py:785-898 with generate_with_fallback :970-1117): every
+    recording of the call stays in ONE batch window after window -- each seek iteration cuts the current 30 s window
+    of every unfinished recording at its own seek (_get_input_segment, zero-padded), encodes them together, decodes
+    them together from the same prompt, and a recording whose seek reaches its length leaves the batch
+    (_maybe_reduce_batch).  Fallback as generate_with_fallback: the rows whose attempt fails HF's gate are decoded
+    again at the next temperature, together; a row is accepted at its first passing attempt (or keeps its last one),
+    and a skipped row advances by its window.  run_eval.py:667-681 calls generate on inner_batch_size recordings this
+    way; HF's own rows are not batch-invariant either (the encoder and the decoder see the batch), so parity is with
+    HF's batched call (tests/test_batched_longform_gpu.py).
+
+    Speculative fallback (fallback_batch, 16-bit paths whose decode rows are independent, batch_rows_independent):
+    while the failing rows are few, several temperature levels of them decode as one batch of at most 8 rows (the
+    decode step at <= 8 rows is one GEMV launch per Linear, latency-bound: extra rows are nearly free); each row still
+    takes its first passing attempt in temperature order, and a row's attempt decodes the same tokens whichever batch
+    it sits in (per-row temperature and seed, tw_select_sample_ts), so the result is the level-by-level one."""
+    model_cfg = model.config
+    dev = model.device
+    nmel = feats.shape[1]
+    B = feats.shape[0]
+    V = model_cfg.vocab_size
+    P = len(init)
+    ml = total_length(model_cfg, gc, P, max_length, max_new_tokens)
+    if P >= ml:
+        raise ValueError(f"prompt of {P} tokens leaves no room below max_length {ml}")
+    ns = (0, ns_token) if no_speech_threshold is not None else None
+    spec = fallback_batch and batch_rows_independent(model)
+    seek = [0] * B
+    nwin = [0] * B
+    outs = [[] for _ in range(B)]
+    while True:
+        active = [b for b in range(B) if seek[b] < int(lens[b])]          # _maybe_reduce_batch
+        if not active:
+            break
+        nfr = {b: min(window, int(lens[b]) - seek[b]) for b in active}
+        # encode the current windows together (chunks of enc_rows bound the encoder's activations)
+        enc = {}
+        for c0 in range(0, len(active), enc_rows):
+            rows = active[c0:c0 + enc_rows]
+            segb = torch.zeros(len(rows), nmel, window, dtype=torch.float32, device=dev)
+            for i, b in enumerate(rows):
+                segb[i, :, :nfr[b]] = feats[b, :, seek[b]:seek[b] + nfr[b]]
+            e = model.encode(model.conv_input(segb))
+            tk = e.shape[0] // len(rows)
+            for i, b in enumerate(rows):
+                enc[b] = e[i * tk:(i + 1) * tk]
+            del segb
+        result = {}                       # b -> (accepted tokens, skip)
+        pending = list(active)
+        level = 0
+        seeds = {b: seeds_of(b, nwin[b]) for b in active}
+        while pending and level < len(temps):
+            per = max(1, 8 // len(pending)) if spec and level > 0 else 1
+            levels = list(range(level, min(len(temps), level + per)))
+            attempts = [(b, f) for f in levels for b in pending]
+            nb = _bucket(len(attempts))
+            pad_n = nb - len(attempts)
+            rows_att = attempts + [attempts[0]] * pad_n
+            one = len({b for b, _ in rows_att}) == 1
+            # the rows' encoder outputs: one window shared by every row (its K/V projected once), else gathered
+            e16 = enc[rows_att[0][0]] if one else torch.cat([enc[b] for b, _ in rows_att])
+            d_ = decoder(P, ml, nb)
+            tl = [temps[f] or 0.0 for _, f in rows_att]
+            sl = [seeds[b][f] for b, f in rows_att]
+            raws = d_.run(e16, torch.tensor([init] * nb, dtype=torch.int64, device=dev),
+                          temperature=tl if nb > 1 else tl[0], seed=sl if nb > 1 else sl[0], no_speech=ns).tolist()
+            del e16
+            # a batch is cut at its LAST row's first eos: each row is cut at its own first eos, what its own decode
+            # returns
+            raws = [row_tokens(r, eos) for r in raws[:len(attempts)]]
+            decided = set()
+            for r, (b, f) in enumerate(attempts):
+                if b in decided:
+                    continue                                  # accepted at a lower temperature of this batch
+                raw = raws[r]
+                cand = trim(raw)
+                needs, skip = False, False
+                if track or compression_ratio_threshold is not None:
+                    tg = time.perf_counter()
+                    avg = float(d_.sel.sum_logp[r]) / max(len(cand), 1) if track else 0.0
+                    nsp = float(torch.exp(d_.ns_logp[r])) if ns is not None else 0.0
+                    needs, skip = need_fallback(cand, avg, nsp, V, compression_ratio_threshold, logprob_threshold,
+                                                no_speech_threshold)
+                    if trace is not None:
+                        trace.append(dict(b=b, seek=seek[b], n=nfr[b], T=temps[f], prompt=list(init), raw=list(raw),
+                                          avg_logprob=avg, no_speech_prob=nsp, needs_fallback=needs, skip=skip,
+                                          batch=nb, gate_ms=(time.perf_counter() - tg) * 1e3))
+                elif trace is not None:
+                    trace.append(dict(b=b, seek=seek[b], n=nfr[b], T=temps[f], prompt=list(init), raw=list(raw),
+                                      batch=nb))
+                result[b] = (raw, skip)
+                if not needs:
+                    decided.add(b)
+            pending = [b for b in pending if b not in decided]
+            level = levels[-1] + 1
+        del enc
+        for b in active:
+            seq, skip = result[b]
+            n = nfr[b]
+            nwin[b] += 1
+            if skip:
+                seek[b] += n
+                continue
+            if seek[b] + window < int(lens[b]) and seq and seq[-1] == eos:    # not the last window: cut its eos
+                seq = seq[:-1]
+            if seq and seq[-1] == pad:                                         # trailing pads (pad == eos keeps one)
+                k = len(seq)
+                while k > 1 and seq[k - 2] == pad:
+                    k -= 1
+                seq = seq[:k] if pad == eos else seq[:k - 1]
+            if not seq:
+                seek[b] += n
+                continue
+            segs, off = retrieve_segment(seq, n, ts_begin)
+            for sgm in segs:
+                outs[b].extend(sgm)
+            seek[b] += off if off > 0 else n          # a closing <|0.00|> pair would not advance: take the window
+    L = max((len(o) for o in outs), default=0)
+    res = torch.full((B, L), pad, dtype=torch.int64)
+    for b, o in enumerate(outs):
+        res[b, :len(o)] = torch.tensor(o, dtype=torch.int64)
+    return res.to(dev)
+
+
 def _longform(model, gc, feats, attention_mask, language, task, max_length, max_new_tokens, use_graph, window,
               trace=None, temperature=0.0, compression_ratio_threshold=None, logprob_threshold=None,
               no_speech_threshold=None, condition_on_prev_tokens=False, seed=0, fallback_batch=True, num_beams=1):
@@ -713,9 +848,16 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
     decoders = {}
 
     def decoder(P, ml, nb=1):
-        if (P, ml, nb) not in decoders:
-            decoders[(P, ml, nb)] = _Decoder(model, gc, nb, cfg.max_source_positions, P, ml, True, use_graph, track)
-        return decoders[(P, ml, nb)]
+        key = (P, ml, nb)
+        if key in decoders:
+            decoders[key] = decoders.pop(key)            # most recently used last
+        else:
+            # each decoder holds a captured step and the cross-attention K/V of its rows (246 MB per row at
+            # large-v2): keep the three most recently used
+            while len(decoders) >= 3:
+                decoders.pop(next(iter(decoders)))
+            decoders[key] = _Decoder(model, gc, nb, cfg.max_source_positions, P, ml, True, use_graph, track)
+        return decoders[key]
 
     def trim(raw):
         cand = list(raw)
@@ -729,40 +871,15 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
     def seeds_of(b, nwin):
         return [(seed * 1000003 + b * 7919 + nwin * 131 + fi) & ((1 << 63) - 1) for fi in range(len(temps))]
 
-    # First windows as batches: every clip's first window has the same prompt, so the first attempt of
-    # up to 8 clips' first windows is encoded and decoded as ONE batch, as HF's seek loop keeps its batch together
-    # (a short-form timestamp call is then one batched decode, not B batch-1 decodes).  Rows are independent on the
-    # 16-bit paths (batch_rows_independent), so each row's tokens and gates are those of its clip's own attempt 0;
-    # the per-clip loop below takes them over and continues (fallback attempts, later windows) clip by clip.
-    first = {}
-    live = [b for b in range(B) if int(lens[b]) > 0]
     nbeam = max(1, int(num_beams or 1))
     beam_ts = (ts_begin, int(gc.no_timestamps_token_id), gc.max_initial_timestamp_index
                if "max_initial_timestamp_index" in gc else None)
-    if len(live) > 1 and batch_rows_independent(model) and nbeam == 1:
-        P0 = len(init)
-        ml0 = total_length(cfg, gc, P0, max_length, max_new_tokens)
-        ns0 = (0, ns_token) if no_speech_threshold is not None else None
-        for c0 in range(0, len(live), 8):
-            rows = live[c0:c0 + 8]
-            nb = len(rows)
-            segb = torch.zeros(nb, nmel, window, dtype=torch.float32, device=dev)
-            for i, b in enumerate(rows):
-                n = min(window, int(lens[b]))
-                segb[i, :, :n] = feats[b, :, :n]
-            enc_all = model.encode(model.conv_input(segb))
-            Tk_ = enc_all.shape[0] // nb
-            d_ = decoder(P0, ml0, nb)
-            tl = [temps[0] or 0.0] * nb
-            sl = [seeds_of(b, 0)[0] for b in rows]
-            raws = d_.run(enc_all, torch.tensor([init] * nb, dtype=torch.int64, device=dev),
-                          temperature=tl if nb > 1 else tl[0], seed=sl if nb > 1 else sl[0], no_speech=ns0).tolist()
-            for i, b in enumerate(rows):
-                raw = row_tokens(raws[i], eos)
-                avg = float(d_.sel.sum_logp[i]) / max(len(trim(raw)), 1) if track else 0.0
-                nsp = float(torch.exp(d_.ns_logp[i])) if ns0 is not None else 0.0
-                first[b] = (raw, avg, nsp, enc_all[i * Tk_:(i + 1) * Tk_], nb)
-
+    if nbeam == 1 and not condition_on_prev_tokens:
+        return _longform_batched(model, gc, feats, lens, init, temps, track, window, trace, max_length,
+                                 max_new_tokens, compression_ratio_threshold, logprob_threshold, no_speech_threshold,
+                                 fallback_batch, decoder, trim, seeds_of, ns_token, ts_begin, eos, pad)
+    # conditioning on the previous windows' text (per-recording prompts of different lengths: HF left-pads them under
+    # a decoder attention mask) and beam search: one recording at a time
     seg_in = torch.zeros(1, nmel, window, dtype=torch.float32, device=dev)
     outs = []
     for b in range(B):
@@ -771,13 +888,9 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
         cond = bool(condition_on_prev_tokens)
         while seek < Tb:
             n = min(window, Tb - seek)
-            pre = first.pop(b, None) if nwin == 0 else None
-            if pre is not None:
-                enc16 = pre[3]
-            else:
-                seg_in.zero_()
-                seg_in[0, :, :n] = feats[b, :, seek:seek + n]
-                enc16 = model.encode(model.conv_input(seg_in))
+            seg_in.zero_()
+            seg_in[0, :, :n] = feats[b, :, seek:seek + n]
+            enc16 = model.encode(model.conv_input(seg_in))
             prompt = list(init)
             if cond and segments and prev_sot is not None:
                 prev = []
@@ -810,9 +923,7 @@ def _longform(model, gc, feats, attention_mask, language, task, max_length, max_
                 grp = rest[fb:fb + per]
                 attempts.append((grp[0], None, None, None, [temps[f] or 0.0 for f in grp], [seeds[f] for f in grp]))
             for fi0, d_, e_, p_, tl, sl in attempts:
-                if fi0 == 0 and pre is not None:             # attempt 0 ran in the first-window batch
-                    raws, gates, nbatch = [pre[0]], [(pre[1], pre[2])], pre[4]
-                elif nbeam > 1 and len(tl) == 1 and not tl[0]:   # temperature 0 with num_beams: the beam search
+                if nbeam > 1 and len(tl) == 1 and not tl[0]:   # temperature 0 with num_beams: the beam search
                     bd = _BeamDecoder(model, gc, 1, nbeam, cfg.max_source_positions, P, ml, timestamps=beam_ts)
                     raw = row_tokens(bd.run(enc16, prompt, no_speech=ns)[0].tolist(), eos)
                     avg = float(bd.sum_logp[0]) / max(len(trim(raw)), 1)

@@ -39,17 +39,12 @@ sys.path.insert(0, REPO)
 from oracle import labels as L  # noqa: E402
 from oracle import logmel  # noqa: E402
 from oracle.weights import CONFIGS, SPECIAL, make_weights  # noqa: E402
+# the fixtures' inputs and settings as plain data, shared with the GPU tests (which import neither this file nor HF)
+from oracle.fixture_inputs import (CFG_CASES, EMBED_STD, LV2_GREEDY_GENERATION, LV2_SEED, ROWS, SUPPRESS,  # noqa: E402,F401
+                                   TS_GENERATION, VSTRIDE, batched_longform_features, cfg_case_batch,
+                                   cfg_case_weights, longform_features, lv2_decode_weights, lv2_features)
 
 REF = "/root/reference"
-# large-v2 generation_config.suppress_tokens (test parameter for the suppress processor)
-SUPPRESS = [1, 2, 7, 8, 9, 10, 14, 25, 26, 27, 28, 29, 31, 58, 59, 60, 61, 62, 63, 90, 91, 92, 93,
-            359, 503, 522, 542, 873, 893, 902, 918, 922, 931, 1350, 1853, 1982, 2460, 2627, 3246,
-            3253, 3268, 3536, 3846, 3961, 4183, 4667, 6585, 6647, 7273, 9061, 9383, 10428, 10929,
-            11938, 12033, 12331, 12562, 13793, 14157, 14635, 15265, 15618, 16553, 16604, 18362,
-            18956, 20075, 21675, 22520, 26130, 26161, 26435, 28279, 29464, 31650, 32302, 32470,
-            36865, 42863, 47425, 49870, 50254, 50258, 50358, 50359, 50360, 50361, 50362]
-ROWS = [0, 3, 4, 57, 200, 446]          # decoder positions whose full logit rows are checked
-VSTRIDE = 97                             # vocab subsample stride for stored logit rows
 
 
 def hf_model(cfg, w, dtype=torch.float32):
@@ -317,19 +312,7 @@ def gen_beam_ts(out):
 
 def ts_generation_config():
     from transformers import GenerationConfig
-    return GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
-                            pad_token_id=SPECIAL["pad"], bos_token_id=SPECIAL["eot"], suppress_tokens=SUPPRESS,
-                            begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=448, num_beams=1,
-                            do_sample=False, no_timestamps_token_id=SPECIAL["notimestamps"], is_multilingual=True,
-                            lang_to_id={"<|en|>": SPECIAL["en"], "<|zh|>": SPECIAL["zh"]},
-                            task_to_id={"transcribe": SPECIAL["transcribe"], "translate": 50358},
-                            max_initial_timestamp_index=50)
-
-
-def longform_features():
-    """Deterministic synthetic log-mel-range features for the long-form fixture (80 x 6500 frames =
-    65 s; feature extraction is pinned separately by mel.npz)."""
-    return (np.random.default_rng(11).standard_normal((1, 80, 6500)) * 0.5).astype(np.float32)
+    return GenerationConfig(**TS_GENERATION)
 
 
 def gen_greedy_ts(out):
@@ -468,69 +451,97 @@ class _MarginSpy:
         return scores
 
 
-LV2_SEED = 61
-
-
-def lv2_features():
-    """Four 30 s synthetic clips (the bench's sine + noise recipe, different seeds and tone lengths) and a 45 s
-    long-form input (the first 4 500 frames of longform_features' deterministic draw)."""
-    short = logmel.log_mel_batch([logmel.synthetic_clip(0), logmel.synthetic_clip(3, 14.0),
-                                  logmel.synthetic_clip(5, 22.0), logmel.synthetic_clip(8, 30.0)])
-    return short, longform_features()[:, :, :4500]
-
-
 def lv2_greedy_config():
     from transformers import GenerationConfig
-    return GenerationConfig(decoder_start_token_id=SPECIAL["sot"], eos_token_id=SPECIAL["eot"],
-                            pad_token_id=SPECIAL["pad"], suppress_tokens=SUPPRESS,
-                            begin_suppress_tokens=[220, SPECIAL["eot"]], max_length=448, num_beams=1, do_sample=False,
-                            no_timestamps_token_id=SPECIAL["notimestamps"])
+    return GenerationConfig(**LV2_GREEDY_GENERATION)
+
+
+def _lv2_tf_logits(m, feats, full_ids, amp):
+    """HF teacher-forced forward: logits [B, T, V] (fp32) of decoder_input_ids = full_ids."""
+    with torch.no_grad(), amp:
+        return m(input_features=feats, decoder_input_ids=full_ids).logits.float()
 
 
 def gen_lv2_decode(out):
     """HF generate at the REAL large-v2 dimensions (d 1280, 32 + 32 layers, 20 heads) -- the model of BASELINE c4 / c5
-    -- with the documented decode-parity weights (oracle/weights.lv2_decode_weights(large-v2, LV2_SEED): the decoder's
-    cross-attention and positions strengthened so that decoding depends on the audio, round 5), in three arithmetics:
+    -- with the round-6 decode-parity weights (oracle/fixture_inputs.lv2_decode_weights(large-v2, LV2_SEED, v_bias):
+    a soft cross-attention whose value path carries each step's attended frames' difference from the mean encoder
+    row; moderate range, audio-dependent, not chaotic -- see LV2_DECODE_SCALES), in three arithmetics:
       f32  fp32 model (mixed_precision "no")
       f16  torch_dtype=float16 model, no autocast (run_eval.py:99, run_pseudo_labelling.py:461-463)
       b16  fp32 model under torch.autocast("cpu", bfloat16) (run_distillation.py:1580-1584: generate_step runs the
            student under the bf16 Accelerator)
-    and these calls:
-      {tag}_greedy_ids / _margin : greedy, 4 clips, [SOT, zh, transcribe, notimestamps], 48 new tokens
-                                   (run_pseudo_labelling.py:917-922 without timestamps)
-      {tag}_ts_ids / _margin     : return_timestamps=True, language zh, 48 new tokens, one clip per call (rows
-                                   padded with -1; margins [step, clip], nan-padded)
-      f32_long_ids, _long_avg_logprobs, _long_ns_probs, _long_margin, _long_window_steps, _long_window_ids : 45 s
-                                   long-form (11 windows, each run to max_length),
-                                   temperature (0.0,), thresholds that never fire, per-window gates (run_eval.py:659-665)
-    _margin = per step and row, the top-1 minus top-2 processed score (_MarginSpy).
-    The committed fixture was made as three processes (LV2_TAGS=f32 and f16 at OMP_NUM_THREADS=4, b16 at 8, then
-    `make_golden.py lv2_merge`): CPU bf16 autocast matmuls depend on the thread count, and at 4 threads one b16 greedy
-    row emits a timestamp pair, after which HF's seek loop decodes a second window for that row even without
-    return_timestamps (a path the engine's decoder_input_ids decode does not take)."""
+    Stored:
+      v_bias                     : [32, 1280] cross-attention value biases, -W_v . e_bar, e_bar = the mean HF fp32
+                                   encoder output row of the four 30 s clips (part of the weight recipe)
+      {tag}_greedy_ids / _margin : free-running greedy, 4 clips, [SOT, zh, transcribe, notimestamps], 48 new tokens
+                                   (run_pseudo_labelling.py:917-922 without timestamps); margin = per step and row,
+                                   top-1 minus top-2 processed score (_MarginSpy)
+      {tag}_ts_ids / _margin     : return_timestamps=True, language zh, 48 new tokens, one clip per call (rows padded
+                                   with -1; margins [step, clip], nan-padded)
+      tf_*                       : TEACHER-FORCED along HF fp32's greedy tokens (one forward over prompt + tokens, the
+                                   logits at the S = 48 predicting positions): tf_len [B] steps up to and including a
+                                   row's eos; tf_top_ids [B, S, 16] the 16 largest PROCESSED (suppress tokens masked,
+                                   begin tokens at step 0) HF fp32 scores; tf_{tag}_vals [B, S, 16] each arithmetic's
+                                   RAW logits at those ids; tf_{tag}_lse [B, S] logsumexp of the raw row;
+                                   tf_{tag}_argmax / _margin [B, S] argmax and top-2 gap of the processed row;
+                                   tf_oracle{16,b16}_vals: the same values from the CPU oracle (oracle/whisper_ref.Ref
+                                   with the engine's 16-bit rounding points) -- the a-priori distance of a correct
+                                   rounding model from HF, recorded beside the tests' bars
+      f32_long_*                 : 45 s long-form (fp32), temperature (0.0,), thresholds that never fire, per-window
+                                   gates and margins (run_eval.py:659-665)"""
     import contextlib
     from transformers.generation.logits_process import LogitsProcessorList
-    from oracle.weights import lv2_decode_weights
+    from oracle.whisper_ref import Ref
     cfg = CONFIGS["large-v2"]
-    w = lv2_decode_weights(cfg, LV2_SEED)
+    d, Ldec = cfg["d_model"], cfg["decoder_layers"]
     short, lf = lv2_features()
     prompt = [SPECIAL["sot"], SPECIAL["zh"], SPECIAL["transcribe"], SPECIAL["notimestamps"]]
-    B = short.shape[0]
-    # LV2_TAGS=f16 (say): only those arithmetics (parallel processes; main() then writes lv2_decode.<tags>.npz, and
-    # `make_golden.py lv2_merge` joins the parts into lv2_decode.npz)
-    tags = os.environ.get("LV2_TAGS", "f32,f16,b16").split(",")
+    P, B, S, K = len(prompt), short.shape[0], 48, 16
+    w = lv2_decode_weights(cfg, LV2_SEED)
+    m = hf_model(cfg, w).eval()
+    with torch.no_grad():
+        enc = m.model.encoder(torch.from_numpy(short)).last_hidden_state
+    ebar = enc.reshape(-1, d).double().mean(0)
+    v_bias = np.stack([-(torch.from_numpy(w[f"model.decoder.layers.{i}.encoder_attn.v_proj.weight"]).double() @ ebar)
+                       .float().numpy() for i in range(Ldec)])
+    out["v_bias"] = v_bias
+    w = lv2_decode_weights(cfg, LV2_SEED, v_bias)
+    del m, enc
+    sup = torch.tensor(LV2_GREEDY_GENERATION["suppress_tokens"])
+
+    def processed(lg):
+        lg = lg.clone()
+        lg[..., sup] = -float("inf")
+        lg[:, 0, [220, SPECIAL["eot"]]] = -float("inf")
+        return lg
+    full = None
     for dt, tag in ((torch.float32, "f32"), (torch.float16, "f16"), (torch.float32, "b16")):
-        if tag not in tags:
-            continue
         m = hf_model(cfg, w, dt).eval()
         amp = torch.autocast("cpu", dtype=torch.bfloat16) if tag == "b16" else contextlib.nullcontext()
         feats = torch.from_numpy(short).to(dt)
         m.generation_config = lv2_greedy_config()
         spy = _MarginSpy()
         with torch.no_grad(), amp:
-            out[f"{tag}_greedy_ids"] = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * B),
-                                                  max_new_tokens=48, logits_processor=LogitsProcessorList([spy])).numpy()
+            ids = m.generate(feats, decoder_input_ids=torch.tensor([prompt] * B), max_new_tokens=S,
+                             logits_processor=LogitsProcessorList([spy])).numpy()
+        out[f"{tag}_greedy_ids"] = ids
         out[f"{tag}_greedy_margin"] = np.stack(spy.steps)
+        if tag == "f32":
+            gen = np.pad(ids, ((0, 0), (0, S - ids.shape[1])), constant_values=SPECIAL["eot"])   # generated ids only
+            out["tf_len"] = np.array([list(r).index(SPECIAL["eot"]) + 1 if SPECIAL["eot"] in r else S for r in gen])
+            full = torch.from_numpy(np.concatenate([np.array([prompt] * B), gen[:, :S - 1]], 1))
+        lg = _lv2_tf_logits(m, feats, full, amp)[:, P - 1:P - 1 + S]            # [B, S, V]
+        pl = processed(lg)
+        if tag == "f32":
+            top = pl.topk(K, dim=-1).indices
+            out["tf_top_ids"] = top.numpy().astype(np.int32)
+        out[f"tf_{tag}_vals"] = torch.gather(lg, -1, top).numpy()
+        out[f"tf_{tag}_lse"] = torch.logsumexp(lg, -1).numpy()
+        t2 = pl.topk(2, dim=-1)
+        out[f"tf_{tag}_argmax"] = t2.indices[..., 0].numpy().astype(np.int32)
+        out[f"tf_{tag}_margin"] = (t2.values[..., 0] - t2.values[..., 1]).numpy()
+        del lg, pl
         m.generation_config = ts_generation_config()
         # one clip per call: HF's timestamp path drops finished rows from its batch (_maybe_reduce_batch), so a
         # batched call's per-step margins cannot be mapped back to clips; rows are padded with -1 / nan
@@ -539,13 +550,13 @@ def gen_lv2_decode(out):
             spy = _MarginSpy()
             with torch.no_grad(), amp:
                 ids_l.append(m.generate(feats[b:b + 1], return_timestamps=True, language="zh", task="transcribe",
-                                        max_new_tokens=48, logits_processor=LogitsProcessorList([spy])).numpy()[0])
+                                        max_new_tokens=S, logits_processor=LogitsProcessorList([spy])).numpy()[0])
             mar_l.append(np.concatenate([s_.reshape(-1) for s_ in spy.steps]))
         L_ = max(len(x) for x in ids_l)
         out[f"{tag}_ts_ids"] = np.stack([np.pad(x, (0, L_ - len(x)), constant_values=-1) for x in ids_l])
         S_ = max(len(x) for x in mar_l)
         out[f"{tag}_ts_margin"] = np.stack([np.pad(x, (0, S_ - len(x)), constant_values=np.nan) for x in mar_l]).T
-        print(tag, "greedy + timestamps done", flush=True)
+        print(tag, "greedy + teacher-forced + timestamps done", flush=True)
         if tag == "f32":
             lt = torch.from_numpy(lf).to(dt)
             kw = dict(attention_mask=torch.ones(1, lt.shape[-1], dtype=torch.long), return_timestamps=True,
@@ -580,12 +591,92 @@ def gen_lv2_decode(out):
             # each window's tokens as HF's gate saw them (seek_sequence), -1-padded [window, token]
             Lw = max(len(r_) for r_ in rec["raw"])
             out[f"{tag}_long_window_ids"] = np.array([r_ + [-1] * (Lw - len(r_)) for r_ in rec["raw"]], dtype=np.int64)
-            # one row per decode step over both windows, in order (batch of one)
+            # one row per decode step over all windows, in order (batch of one)
             out[f"{tag}_long_margin"] = np.concatenate([s_.reshape(-1) for s_ in spy.steps])
             print(tag, "long-form done", flush=True)
         del m
+    # the CPU oracle with the engine's rounding points, teacher-forced along the same tokens
+    wt = {k: torch.from_numpy(v) for k, v in w.items()}
+    for name, kw in (("oracle16", dict(amp=True, stream_bf16=True, half=torch.float16)),
+                     ("oracleb16", dict(amp=True, stream_bf16=False, half=torch.bfloat16))):
+        ref = Ref(cfg, wt, **kw)
+        with torch.no_grad():
+            lg = ref.forward(feats=torch.from_numpy(short), decoder_input_ids=full)["logits"][:, P - 1:P - 1 + S]
+        out[f"tf_{name}_vals"] = torch.gather(lg, -1, top).numpy()
+        print(name, "done", flush=True)
     out["prompt"] = np.array(prompt)
     out["seed"] = np.int64(LV2_SEED)
+
+
+def gen_batched_longform(out):
+    """HF's BATCHED sequential long-form generate (generation_whisper.py:785-898 + generate_with_fallback :970-1117):
+    ONE generate call on 3 recordings of different lengths (oracle/fixture_inputs.batched_longform_features: 65 s,
+    41.3 s, 18.2 s, attention mask), the call of run_eval.py:667-681 (return_timestamps, language zh, temperature
+    (0.0,), thresholds that never fire so every window's gates are recorded but none falls back), in fp32 at
+      micro  the timestamp fixture's micro model (make_weights(micro, 1, lin_std=0.2), greedy_ts.npz)
+      lv2    the large-v2 decode-parity model (lv2_decode_weights with lv2_decode.npz's v_bias)
+    Stored per {dims}: bl_{dims}_ids (the call's output, pad-padded); per decoded window in HF's order (seek iteration,
+    then batch row): bl_{dims}_win_b (recording), _win_seek (frame), _win_ids (the tokens HF's gate saw, -1-padded),
+    _win_avg / _win_ns (average log-prob, no-speech probability), _win_margin (per step top-1 minus top-2 processed
+    score, nan-padded); the batch of each iteration is recorded by spying on _maybe_reduce_batch."""
+    from transformers.generation.logits_process import LogitsProcessorList, WhisperNoSpeechDetection
+    feats, mask = batched_longform_features()
+    lv2 = np.load(os.path.join(HERE, "lv2_decode.npz"))
+    for dims in os.environ.get("BL_DIMS", "micro,lv2").split(","):
+        if dims == "micro":
+            cfg = CONFIGS["micro"]
+            m = hf_model(cfg, make_weights(cfg, 1, lin_std=0.2)).eval()
+        else:
+            cfg = CONFIGS["large-v2"]
+            m = hf_model(cfg, lv2_decode_weights(cfg, int(lv2["seed"]), lv2["v_bias"])).eval()
+        m.generation_config = ts_generation_config()
+        cls = type(m)
+        orig_need, orig_red = cls._need_fallback, cls._maybe_reduce_batch
+        rec = {"b": [], "seek": [], "ids": [], "avg": [], "ns": [], "margin": []}
+        it = {"map": None, "seek": None, "start": 0}
+        spy = _MarginSpy()
+
+        def red_spy(input_features, seek, max_frames, cur_bsz, batch_idx_map):
+            r = orig_red(input_features, seek, max_frames, cur_bsz, batch_idx_map)
+            it["map"], it["seek"], it["start"] = list(r[2]), seek.clone(), len(spy.steps)
+            return r
+
+        def need_spy(self, seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size,
+                     temperature):
+            b = it["map"][index]
+            rec["b"].append(b)
+            rec["seek"].append(int(it["seek"][b]))
+            rec["ids"].append([int(t) for t in seek_sequence.tolist()])
+            rec["avg"].append(float(self._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence,
+                                                                temperature)))
+            for p_ in logits_processor or []:
+                if isinstance(p_, WhisperNoSpeechDetection):
+                    rec["ns"].append(float(p_.no_speech_prob[index]))
+            steps = spy.steps[it["start"]:]
+            rec["margin"].append(np.array([s_[index] for s_ in steps[:len(seek_outputs[index]["scores"])]],
+                                          dtype=np.float32))
+            return orig_need(self, seek_sequence, seek_outputs, index, logits_processor, generation_config,
+                             vocab_size, temperature)
+        cls._need_fallback, cls._maybe_reduce_batch = need_spy, staticmethod(red_spy)
+        try:
+            with torch.no_grad():
+                ids = m.generate(torch.from_numpy(feats), attention_mask=torch.from_numpy(mask), return_timestamps=True,
+                                 language="zh", task="transcribe", temperature=(0.0,), logprob_threshold=-1e9,
+                                 no_speech_threshold=1.0, logits_processor=LogitsProcessorList([spy])).numpy()
+        finally:
+            cls._need_fallback, cls._maybe_reduce_batch = orig_need, staticmethod(orig_red)
+        k = f"bl_{dims}"
+        out[f"{k}_ids"] = ids
+        out[f"{k}_win_b"] = np.array(rec["b"], dtype=np.int64)
+        out[f"{k}_win_seek"] = np.array(rec["seek"], dtype=np.int64)
+        Lw = max(len(r_) for r_ in rec["ids"])
+        out[f"{k}_win_ids"] = np.array([r_ + [-1] * (Lw - len(r_)) for r_ in rec["ids"]], dtype=np.int64)
+        out[f"{k}_win_avg"] = np.array(rec["avg"], dtype=np.float64)
+        out[f"{k}_win_ns"] = np.array(rec["ns"], dtype=np.float64)
+        Ls = max(len(x) for x in rec["margin"])
+        out[f"{k}_win_margin"] = np.stack([np.pad(x, (0, Ls - len(x)), constant_values=np.nan) for x in rec["margin"]])
+        print(dims, "windows", list(zip(rec["b"], rec["seek"])), flush=True)
+        del m
 
 
 # ------------------------------------------------------------------------------------------------
@@ -597,49 +688,6 @@ def gen_lv2_decode(out):
 # returns LN of a bf16 stream in bf16 where CUDA returns fp32, identical once the next Linear casts
 # it), the teacher's weights in bf16 (teacher_dtype, :1011-1018).  The fp32 model (mixed_precision
 # "no") is stored beside it.
-EMBED_STD = 0.05
-CFG_CASES = {
-    # c1: tiny <- tiny, B 2, launcher flags (freeze_encoder -> shared encoder, frozen decoder positions)
-    "c1": dict(student="tiny", teacher="tiny", s_seed=31, t_seed=32, B=2, freeze_encoder=True,
-               freeze_embed_positions=True, label_seed=41, secs=[30.0, 17.0]),
-    # c2: small <- large-v2 (d 768 vs 1280: no sharing, full teacher forward), every student weight
-    # trainable incl. the conv stem and encoder (240.6 M trainable)
-    "c2": dict(student="small", teacher="large-v2", s_seed=33, t_seed=34, B=1, freeze_encoder=False,
-               freeze_embed_positions=False, label_seed=42, secs=[30.0]),
-    # c3: distil-32-2 made by create_student_model from the large-v2 teacher (decoder layers 0 and 31),
-    # frozen shared encoder, a <|startofprev|> prompt (A7 teacher-input quirk at full size)
-    "c3": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=1, freeze_encoder=True,
-               freeze_embed_positions=True, label_seed=43, secs=[30.0], prompt=True),
-    # c3 at B = 10: encoder rows 15 000 and decoder rows 4 470, the encoder projections on the persistent kernel of
-    # the B = 64 step
-    "c3b10": dict(student=None, teacher="large-v2", s_seed=None, t_seed=34, B=10, freeze_encoder=True,
-                  freeze_embed_positions=True, label_seed=45, secs=[30.0, 27.5, 12.0, 30.0, 8.0, 19.0, 30.0, 24.0,
-                                                                    30.0, 15.5], prompt=True),
-}
-
-
-def cfg_case_weights(case):
-    """(student cfg, student weights, teacher cfg, teacher weights) of a BASELINE-config case."""
-    from oracle.student_ref import init_student_from_teacher
-    c = CFG_CASES[case]
-    tcfg = CONFIGS[c["teacher"]]
-    wt = make_weights(tcfg, c["t_seed"], per_tensor=True, embed_std=EMBED_STD)
-    if c["student"] is None:
-        scfg, ws, _, _ = init_student_from_teacher(tcfg, wt, decoder_layers=2)
-    else:
-        scfg = CONFIGS[c["student"]]
-        ws = make_weights(scfg, c["s_seed"], per_tensor=True, embed_std=EMBED_STD)
-    return scfg, ws, tcfg, wt
-
-
-def cfg_case_batch(case):
-    c = CFG_CASES[case]
-    feats = logmel.log_mel_batch([logmel.synthetic_clip(i, c["secs"][i]) for i in range(c["B"])])
-    lists = L.synthetic_label_lists(c["B"], seed=c["label_seed"], prompt_fraction=0.0)
-    if c.get("prompt"):
-        lists[0] = [SPECIAL["startofprev"]] + list(range(300, 340)) + lists[0][:300]
-    dec, lab = L.collate(lists)
-    return feats, dec, lab
 
 
 def _trainable(names, freeze_encoder, freeze_embed_positions):
@@ -727,7 +775,7 @@ def main():
     only = sys.argv[1:]
     for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy), ("beam", gen_beam), ("beam_ts", gen_beam_ts),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
-                     ("lv2_decode", gen_lv2_decode),
+                     ("lv2_decode", gen_lv2_decode), ("batched_longform", gen_batched_longform),
                      ("cfg_c1", lambda o: gen_cfg("c1", o)), ("cfg_c2", lambda o: gen_cfg("c2", o)),
                      ("cfg_c3", lambda o: gen_cfg("c3", o)), ("cfg_c3b10", lambda o: gen_cfg("c3b10", o))):
         if only and name not in only:

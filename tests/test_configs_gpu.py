@@ -47,8 +47,7 @@ def _gpu():
 
 def _case(name):
     import sys, os
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    import make_golden as mg
+    import oracle.fixture_inputs as mg
     return mg
 
 

@@ -242,14 +242,9 @@ def test_generate_graph_replay_equals_eager():
 
 def _ts_model():
     import os, sys
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    import make_golden as mg
+    import oracle.fixture_inputs as mg
     cfg, w, m, GC = _micro()
-    gc = mg.ts_generation_config().to_dict()
-    m.generation_config = GC({k: gc[k] for k in ("decoder_start_token_id", "eos_token_id", "pad_token_id",
-                                                  "suppress_tokens", "begin_suppress_tokens", "max_length",
-                                                  "no_timestamps_token_id", "is_multilingual", "lang_to_id",
-                                                  "task_to_id", "max_initial_timestamp_index")})
+    m.generation_config = GC({k: mg.TS_GENERATION[k] for k in mg.TW_GENERATION_KEYS})
     return mg, cfg, w, m
 
 

@@ -173,7 +173,6 @@ def test_checkpoint_resume_and_reference_optimizer_interop(tmp_path):
     (1) resume == uninterrupted training (same kernels, same inputs);
     (2) optimizer.bin loads into the reference's torch AdamW over HF named_parameters() groups and
         the per-parameter moments equal ours; a torch-written optimizer.bin loads back into ours."""
-    import transformers
     from safetensors.torch import load_file
     from oracle import distill_ref
     from oracle.weights import CONFIGS
@@ -203,20 +202,22 @@ def test_checkpoint_resume_and_reference_optimizer_interop(tmp_path):
     for n in sorted(s.trainable):
         x, y = s.state_view(n).float(), s2.state_view(n).float()
         assert torch.allclose(x, y, rtol=1e-6, atol=1e-7), n
-    # (2) the reference's optimizer over an HF model built from model.safetensors
+    # (2) the reference's torch AdamW over the HF model's named_parameters() built from model.safetensors: the
+    # parameters as plain tensors in HF registration order (tw.checkpoint.hf_parameter_names, pinned equal to
+    # transformers' own named_parameters() order by tests/test_checkpoint_cpu.py::test_hf_parameter_order; the tied
+    # proj_out is de-duplicated there as in HF), so this GPU test needs no transformers import
+    from tw.checkpoint import hf_parameter_names
+    from tw.config import WhisperConfig
     cfg = CONFIGS["micro"]
-    hf = transformers.WhisperForConditionalGeneration(transformers.WhisperConfig(**cfg))
-    missing, unexpected = hf.load_state_dict(load_file(str(ck / "model.safetensors")), strict=False)
-    assert missing == ["proj_out.weight"] and unexpected == []
-    for n, p in hf.named_parameters():
-        p.requires_grad_(n in s.trainable)
-    names = [n for n, _ in hf.named_parameters()]
+    sd = load_file(str(ck / "model.safetensors"))
+    names = hf_parameter_names(WhisperConfig(**cfg))
+    assert sorted(sd) == sorted(names)
+    byname = {n: torch.nn.Parameter(sd[n].clone(), requires_grad=n in s.trainable) for n in names}
     decay = set(distill_ref.decay_parameter_names(names, ("model.encoder.",)))
-    opt = torch.optim.AdamW([dict(params=[p for n, p in hf.named_parameters() if n in decay], weight_decay=0.01),
-                             dict(params=[p for n, p in hf.named_parameters() if n not in decay], weight_decay=0.0)],
+    opt = torch.optim.AdamW([dict(params=[byname[n] for n in names if n in decay], weight_decay=0.01),
+                             dict(params=[byname[n] for n in names if n not in decay], weight_decay=0.0)],
                             lr=1e-3)
     opt.load_state_dict(torch.load(str(ck / "optimizer.bin"), weights_only=True))
-    byname = dict(hf.named_parameters())
     from tw.modeling import to_hf
     for n in names:
         st = opt.state.get(byname[n], {})

@@ -143,3 +143,58 @@ def test_dp_deferred_update_bit_identical():
         for x, y in zip(a, b):
             assert torch.equal(x, y)
     assert torch.equal(out[0][True][0], out[1][True][0])
+
+
+def _worker_rccl(rank, world, port, out):
+    """One rank on a real `nccl` (= RCCL) process group with the exchange forced on (force_exchange): per-layer async
+    all-reduces issued from the backward hook, the tail, Work.wait() on the compute stream and the deferred AdamW
+    (overlap_update) all run on the backend of the 8-GPU node; the same steps without a process group beside it."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    torch.distributed.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    mk, g = _setup()
+    from tw.distill import DistillationTrainer
+    B = g["feats"].shape[0]
+    res = {}
+    for dp in (True, False):
+        s, t = mk(1, torch.float32), mk(2, torch.bfloat16)
+        kw = dict(process_group=torch.distributed.group.WORLD, force_exchange=True, overlap_update=True) if dp else {}
+        tr = DistillationTrainer(s, t, learning_rate=1e-3, freeze_encoder=True, dp_bucket_mb=1, **kw)
+        launched = []
+        if dp:
+            tr.exchange_log, tr.exchange_events = [], []
+            orig = tr._grad_ready
+            tr._grad_ready = lambda p, orig=orig: (launched.append(p), orig(p))
+        for it in range(3):
+            tr.train_step(_batch(g, it % B, it % B + 1))
+            if dp:
+                assert tr._update is not None        # the update waits for the next step's encoder
+        sd = tr.state_dict()                          # flushes
+        torch.cuda.synchronize()
+        res[dp] = (s.store.p32.cpu().clone(), sd["exp_avg"].cpu().clone(), sd["exp_avg_sq"].cpu().clone(),
+                   list(launched), list(tr.exchange_log or []), len(tr.exchange_events or []),
+                   torch.distributed.get_backend() if dp else None)
+    out[rank] = res
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_rccl_one_rank_bit_identical():
+    """the RCCL code path on one GPU.  DistillationTrainer on an `nccl` process group of world size
+    1 with the exchange forced on and the deferred update: after 3 steps the weights and AdamW moments are
+    bit-identical to the trainer without a process group (an all-reduce over one rank is the identity), every decoder
+    layer's exchange started inside the backward, and the tail went out after it."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    out = mp.Manager().dict()
+    mp.spawn(_worker_rccl, args=(1, _free_port(), out), nprocs=1, join=True)
+    dp, ref = out[0][True], out[0][False]
+    for x, y in zip(dp[:3], ref[:3]):
+        assert torch.equal(x, y)
+    launched, log, nwait, backend = dp[3], dp[4], dp[5], dp[6]
+    assert backend == "nccl"
+    assert any(p.startswith("model.decoder.layers.") for p in launched)
+    assert any(not tail for _, tail in log) and any(tail for _, tail in log)
+    assert nwait == 3

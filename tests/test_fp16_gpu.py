@@ -195,14 +195,9 @@ def _model(lin_std=0.02, ts=False):
     m = WhisperForConditionalGeneration.from_state_dict(WhisperConfig(**cfg), {k: torch.from_numpy(v) for k, v in
                                                                               w.items()}, dtype=torch.float16)
     assert m.compute == "fp16" and m.act_dtype == torch.float16 and m.store.p16.dtype == torch.float16
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    import make_golden as mg
+    import oracle.fixture_inputs as mg
     if ts:
-        gc = mg.ts_generation_config().to_dict()
-        m.generation_config = GenerationConfig({k: gc[k] for k in (
-            "decoder_start_token_id", "eos_token_id", "pad_token_id", "suppress_tokens", "begin_suppress_tokens",
-            "max_length", "no_timestamps_token_id", "is_multilingual", "lang_to_id", "task_to_id",
-            "max_initial_timestamp_index")})
+        m.generation_config = GenerationConfig({k: mg.TS_GENERATION[k] for k in mg.TW_GENERATION_KEYS})
     else:
         m.generation_config = GenerationConfig(suppress_tokens=mg.SUPPRESS, begin_suppress_tokens=[220, 50257])
     return m, mg
@@ -295,8 +290,7 @@ def _oracle_avg(lf, t):
     from oracle import greedy_ref
     from oracle.weights import CONFIGS, make_weights
     from oracle.whisper_ref import Ref, to_torch
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    import make_golden as mg
+    import oracle.fixture_inputs as mg
     cfg = CONFIGS["micro"]
     ref = Ref(cfg, to_torch(make_weights(cfg, 1, lin_std=0.2), torch.float16), amp=True, stream_bf16=True,
               half=torch.float16)

@@ -245,8 +245,7 @@ def test_fp32_train_step_matches_hf_fp32_micro():
 def test_fp32_train_step_matches_hf_fp32_c1():
     """c1 dims (tiny <- tiny, B 2, shared frozen encoder): the fp32 engine vs HF fp32."""
     import os, sys
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    import make_golden as mg
+    import oracle.fixture_inputs as mg
     g = load_golden("cfg_c1")
     scfg, ws, tcfg, wt = mg.cfg_case_weights("c1")
     feats, dec, lab = mg.cfg_case_batch("c1")
@@ -271,8 +270,7 @@ def test_fp32_train_step_matches_hf_fp32_large(name):
     (distil-32-2 made by tw.student from the large-v2 teacher, shared frozen encoder, prompt quirk) at B=1
     on the fp32 path vs HF fp32."""
     import os, sys
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    import make_golden as mg
+    import oracle.fixture_inputs as mg
     from oracle.weights import CONFIGS, make_weights
     from tw.config import WhisperConfig
     from tw.modeling import WhisperForConditionalGeneration

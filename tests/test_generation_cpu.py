@@ -31,10 +31,12 @@ class _ScriptedDecoder:
         self.ns_logp = torch.zeros(nb)
 
     def run(self, enc16, prompt, temperature=0.0, seed=0, no_speech=None):
-        win = int(enc16.flatten()[0].item())
+        # one encoder row per window here: nb rows (one per decode row), or one row shared by every decode row
+        ids = enc16.flatten()
+        wins = [int(ids[r].item()) if ids.numel() == self.nb else int(ids[0].item()) for r in range(self.nb)]
         temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
         assert len(temps) == self.nb
-        rows = [list(self.script[(win, round(t, 1))]) for t in temps]
+        rows = [list(self.script[(w, round(t, 1))]) for w, t in zip(wins, temps)]
         L = max(len(r) for r in rows)
         for i, r in enumerate(rows):
             self.sel.sum_logp[i] = -0.1 * len(r)
@@ -45,7 +47,7 @@ def _model():
     cfg = types.SimpleNamespace(max_source_positions=1500, max_target_positions=448, vocab_size=51865, d_model=128)
     m = types.SimpleNamespace(config=cfg, device=torch.device("cpu"), compute="bf16")
     m.conv_input = lambda feats: feats
-    m.encode = lambda x: x[:, :1, :1].reshape(1, 1).clone()     # the window id the features carry
+    m.encode = lambda x: x[:, :1, :1].reshape(-1, 1).clone()    # the window id the features carry, one row a window
     return m
 
 
@@ -79,6 +81,37 @@ def test_batched_fallback_row_finishing_first_equals_sequential(monkeypatch):
     # window 0 accepted at T = 0.2 (its predicted eos cut: not the last window), window 1 at T = 0 (final: eos kept)
     assert a == [TS0, 100, 101, TS0 + 100, TS0, 400, 401, TS0 + 50, EOS]
     assert EOS not in a[:-1]
+
+
+def test_batched_recordings_stay_together(monkeypatch):
+    """HF's batched long-form (generation_whisper.py:785-898): two recordings of different lengths decode their
+    current windows as ONE batch per seek iteration; the failing row alone falls back (its remaining temperatures
+    speculatively batched), the finished recording leaves the batch, and each recording's tokens are what it gets
+    decoded on its own."""
+    monkeypatch.setattr(generation, "_Decoder", _ScriptedDecoder)
+    script = _script()
+    script[(2, 0.0)] = [TS0, 500, 501, TS0 + 20, EOS]
+    _ScriptedDecoder.script = script
+    feats = torch.zeros(2, 80, 6000)
+    feats[0, :, 3000:] = 1.0                                      # recording 0: windows 0, 1
+    feats[1] = 2.0                                                # recording 1: one 25 s window (id 2)
+    mask = torch.ones(2, 6000, dtype=torch.long)
+    mask[1, 2500:] = 0
+    gc = GenerationConfig(decoder_start_token_id=50258, eos_token_id=EOS, pad_token_id=EOS,
+                          no_timestamps_token_id=50363, suppress_tokens=[], lang_to_id={"<|zh|>": 50260})
+    trace = []
+    out = generation._longform(_model(), gc, feats, mask, "zh", "transcribe", None, 40, False, 3000, trace,
+                               temperature=(0.0, 0.2, 0.4, 0.6), compression_ratio_threshold=1.35)
+    assert out[0].tolist() == [TS0, 100, 101, TS0 + 100, TS0, 400, 401, TS0 + 50, EOS]
+    assert out[1].tolist()[:5] == [TS0, 500, 501, TS0 + 20, EOS] and set(out[1].tolist()[5:]) <= {EOS}
+    first = [t for t in trace if t["T"] == 0.0 and t["seek"] == 0]
+    assert [t["b"] for t in first] == [0, 1] and all(t["batch"] == 2 for t in first)
+    fb = [t for t in trace if t["T"] > 0]
+    assert {t["b"] for t in fb} == {0} and all(t["batch"] == 4 for t in fb)     # 3 temperatures, padded to 4 rows
+    later = [t for t in trace if t["seek"] > 0]
+    assert [t["b"] for t in later] == [0] and later[0]["batch"] == 1            # recording 1 left the batch
+    solo0, _ = _run(monkeypatch, True, _script())
+    assert out[0].tolist() == solo0
 
 
 def test_row_tokens():

@@ -709,11 +709,14 @@ def test_logmel_longform_matches_oracle_and_hf():
 
 # ----------------------------------------------------------------------------- decode GEMV
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("N,K,ln", [(1280, 1280, True), (3840, 1280, False), (1280, 5120, False)])
+@pytest.mark.parametrize("N,K,ln", [(1280, 1280, True), (3840, 1280, False), (1280, 5120, False), (51865, 1280, True),
+                                    (51904, 1280, True)])
 def test_gemv_rows_independent_of_batch(dt, N, K, ln):
     """Each row of an M-row GEMV (M = 2..8, the fallback batch of a long-form window) is bit-identical to the
     same row decoded alone (M = 1): tw.generation.batch_rows_independent relies on it to decode the remaining
-    temperatures of a window as one batch.  Covers the fused LayerNorm, bias, GELU and residual epilogues."""
+    temperatures of a window as one batch.  Covers the fused LayerNorm, bias, GELU and residual epilogues, and the
+    LM-head instantiations (N >= 16384: 4 columns per wave at 1 and 5..8 rows, 8 at 2..4; N = 51865 has a ragged
+    column tail)."""
     from tw import ops
     g = torch.Generator().manual_seed(N + K)
     x = (torch.randn(8, K, generator=g) * 2 + 0.3).to(dt).to(DEV)
