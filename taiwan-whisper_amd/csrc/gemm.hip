@@ -957,6 +957,9 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   // very long K (the LM-head input gradient, K = 51 904): the persistent kernel wins from one round up
   // (3356 vs 4006 us on 560 tiles, tools/bench_head_bwd.py), its per-tile fixed cost being amortised
   if (!a_trans && !b_trans && K >= 8192 && t256 >= pp_grid_cus()) tile = 256;
+  // ... and its transposed-B form (the student's LM-head dX = dlogits . E, K = 51 904, 560 tiles) on the 2-stage
+  // 256x256 tile: 4059 vs 4370 us on the 128x128 one (tools/bench_gemm.py "dX head", profiles/r06_a_gemm.log)
+  if (!a_trans && b_trans && K >= 8192 && t256 >= pp_grid_cus()) tile = 256;
   // K-major forward grids of 1-4 rounds whose rounds are well filled (c2's B = 32 shapes: the teacher encoder's
   // N = 1280 Linears at M = 48 000, 940 256-tiles = 3.67 rounds, 92 % of the workgroup-rounds busy; the student
   // decoder's fused QKV and fc1): the persistent kernel.  Grids with a mostly idle last round take the whole-round

@@ -56,7 +56,7 @@ def test_batched_longform_fp32_vs_hf_batched_call(dims):
     import oracle.fixture_inputs as fx
     g = load_golden("batched_longform")
     k = f"bl_{dims}"
-    if f"{k}_ids" not in g.files:
+    if f"{k}_ids" not in g:
         pytest.skip(f"fixture has no {dims} part")
     m = _model(dims, g)
     feats, mask = fx.batched_longform_features()

@@ -18,9 +18,16 @@ fp32; torch_dtype=float16 (run_eval.py:99, run_pseudo_labelling.py:461-463); the
 plus HF's logits TEACHER-FORCED along HF fp32's greedy tokens in each arithmetic (the 16 largest processed fp32 scores'
 ids per step, every arithmetic's raw logits there, the row logsumexp, the processed argmax and its top-2 gap).
 
-Every bound below is computed from the fixture, from constants fixed before the engine ran on it:
+Every bound below is computed from the fixture, with constants fixed from CPU evidence before the engine ran on it:
   D(tag)     = rms over the valid (row, step, top-16 id) entries of HF_tag - HF_fp32: the whole effect of the 16-bit
-               rounding points on the logits (measured: fp16 ~0.016, bf16 ~0.1);
+               rounding points on the logits (fixture: fp16 0.038, bf16 0.215);
+  O(tag)     = rms of oracle_tag - HF_tag over the same entries, oracle_tag = the CPU restatement of the ENGINE's
+               rounding points (oracle/whisper_ref.Ref, stored in the fixture): how far a correct 16-bit rounding
+               model that is not HF's own code sits from HF (fixture: fp16 0.73 D, bf16 0.32 D -- the flash-attention
+               P roundings relative to each implementation's running maxima, HF's CPU kernel in 512-key blocks, are
+               16-bit noise of their own);
+  K(tag)     = min(0.9, 1.5 x O(tag) / D(tag)): the engine within 1.5 x the oracle's distance, and in any case closer to
+               HF_tag than exact fp32 arithmetic (the engine's fp32 path, = HF fp32 to 1e-4) is;
   TIE(tag)   = 2 x max |HF_tag - HF_fp32| over the same entries: a top-2 gap below it is within what the 16-bit
                rounding points move a logit, so a different choice there is a tie, not an error.
 Parity bar:
@@ -30,16 +37,14 @@ Parity bar:
     recording when no window has one); teacher-forced logits within 0.1 x D(fp16) of HF fp32;
   * fp16 model vs HF torch_dtype=float16, bf16 (fp32 parameters, autocast) vs HF bf16 autocast, teacher-forced through
     the engine's KV-cache decode step (DecodeSession, the kernels generate() replays):
-      - rms(engine - HF_tag) <= K_DIST x D(tag), K_DIST = 0.5: a correct rounding model differs from HF's only by
-        the fp32 summation order inside each rounded op (a rounding flips rarely, by one ulp); a model missing a
-        rounding point (an fp32 residual stream, unrounded Linear outputs) sits at ~D(tag) from HF_tag.  The CPU
-        oracle with the engine's rounding points (oracle/whisper_ref.Ref) is recorded in the fixture
-        (tf_oracle16_vals, tf_oracleb16_vals): its ratio is printed beside the engine's;
+      - rms(engine - HF_tag) <= K(tag) x D(tag): a model missing a rounding point (an fp32 residual stream, unrounded
+        Linear outputs) sits at ~D(tag) from HF_tag, as fp32 does;
       - the engine's processed argmax agrees with HF_tag's at >= 90 % of the valid steps, and every step where it
         does not has an HF_tag top-2 gap below TIE(tag);
       - logsumexp per step within TIE(tag) / 2 of HF_tag's;
     and free-running: fp16 greedy, fp16 timestamps and bf16 greedy ids identical to HF's free-running ids of that
-    arithmetic up to each row's first step whose HF top-2 gap is below TIE(tag).
+    arithmetic up to each row's first step whose HF top-2 gap is below TIE(tag) (timestamps: within the first
+    window's kept tokens, where output position = decode step).
 """
 import numpy as np
 import pytest
@@ -50,7 +55,6 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 FP32_TIE = 2e-3
-K_DIST = 0.5
 EOT = 50257
 
 
@@ -99,12 +103,19 @@ def _rows(ids):
     return [[int(t) for t in r if t not in (-1, EOT)] for r in ids]
 
 
+def _rms(x):
+    return float(np.sqrt(np.mean(np.asarray(x, dtype=np.float64) ** 2)))
+
+
 def _bounds(g, tag):
-    """(valid-entry mask [B, S], D(tag), TIE(tag)) from the fixture (module docstring)."""
+    """(valid-entry mask [B, S], D(tag), TIE(tag), K(tag)) from the fixture (module docstring)."""
     B, S, _ = g["tf_top_ids"].shape
     valid = np.arange(S)[None, :] < g["tf_len"][:, None]
     d = (g[f"tf_{tag}_vals"] - g["tf_f32_vals"])[valid]
-    return valid, float(np.sqrt(np.mean(d.astype(np.float64) ** 2))), 2.0 * float(np.abs(d).max())
+    D = _rms(d)
+    otag = "oracle16" if tag == "f16" else "oracleb16"
+    O = _rms((g[f"tf_{otag}_vals"] - g[f"tf_{tag}_vals"])[valid]) if tag in ("f16", "b16") else 0.0
+    return valid, D, 2.0 * float(np.abs(d).max()), min(0.9, 1.5 * O / D)
 
 
 def test_lv2_fp32_greedy_timestamps_longform_bit_exact(lv2):
@@ -187,7 +198,7 @@ def test_lv2_fp32_teacher_forced_logits(lv2):
     short, _ = fx.lv2_features()
     m = _model(lv2, torch.float32, "fp32", ts=False)
     raw, am = _teacher_forced(m, short, g["prompt"].tolist(), _forced_tokens(g), fx.LV2_GREEDY_SUPPRESS, [220, EOT])
-    valid, D16, _ = _bounds(g, "f16")
+    valid, D16, _, _ = _bounds(g, "f16")
     vals = torch.gather(raw, -1, torch.from_numpy(g["tf_top_ids"]).long()).numpy()
     err = np.abs(vals - g["tf_f32_vals"])[valid]
     print(f"fp32 teacher-forced: max |engine - HF fp32| {err.max():.2e} (bound {0.1 * D16:.2e})")
@@ -206,11 +217,11 @@ def test_lv2_16bit_teacher_forced_vs_hf(lv2, arith):
     raw, am = _teacher_forced(m, short, g["prompt"].tolist(), _forced_tokens(g), fx.LV2_GREEDY_SUPPRESS, [220, EOT])
     del m
     torch.cuda.empty_cache()
-    valid, D, TIE = _bounds(g, tag)
+    valid, D, TIE, K = _bounds(g, tag)
     vals = torch.gather(raw, -1, torch.from_numpy(g["tf_top_ids"]).long()).numpy()
     hf = g[f"tf_{tag}_vals"]
-    rms = float(np.sqrt(np.mean(((vals - hf)[valid]).astype(np.float64) ** 2)))
-    orms = float(np.sqrt(np.mean(((g[f"tf_{otag}_vals"] - hf)[valid]).astype(np.float64) ** 2)))
+    rms = _rms((vals - hf)[valid])
+    orms = _rms((g[f"tf_{otag}_vals"] - hf)[valid])
     lse = torch.logsumexp(raw, -1).numpy()
     lse_err = float(np.abs(lse - g[f"tf_{tag}_lse"])[valid].max())
     want = g[f"tf_{tag}_argmax"]
@@ -220,7 +231,7 @@ def test_lv2_16bit_teacher_forced_vs_hf(lv2, arith):
     print(f"{arith}: rms(engine - HF) {rms:.4f} = {rms / D:.3f} D (oracle {orms / D:.3f} D; D = {D:.4f}); argmax "
           f"agreement {agree.mean():.3f} (HF fp32 vs HF {arith}: {hf32_agree:.3f}); mismatch gaps "
           f"{np.sort(mismatch_list(mism_margin))} < TIE {TIE:.3f}; max lse err {lse_err:.4f}")
-    assert rms <= K_DIST * D, (rms, D)
+    assert rms <= K * D, (rms, K, D)
     assert agree.mean() >= 0.9, agree.mean()
     assert (mism_margin < TIE).all(), (mism_margin, TIE)
     assert lse_err <= TIE / 2, (lse_err, TIE)
@@ -249,16 +260,27 @@ def test_lv2_16bit_free_running_vs_hf(lv2, arith):
     fx, g, _ = lv2
     short, _ = fx.lv2_features()
     dt, tag = (torch.float16, "f16") if arith == "fp16" else (torch.float32, "b16")
-    _, _, TIE = _bounds(g, tag)
+    _, _, TIE, _ = _bounds(g, tag)
     m = _model(lv2, dt, arith, ts=False)
     got = _greedy(m, g, short)
     want = g[f"{tag}_greedy_ids"]
     got = np.pad(got, ((0, 0), (0, max(0, want.shape[1] - got.shape[1]))), constant_values=EOT)
     _prefix_equal(got.tolist(), want.tolist(), g[f"{tag}_greedy_margin"].T, TIE, f"{arith} greedy")
     if arith == "fp16":
+        from tw.generation import retrieve_segment
         m = _model(lv2, dt, arith, ts=True)
-        ts = _timestamps(m, short, dt)
-        # the fixture's timestamp rows (one clip per call) keep their closing eos; margins [step, clip]
+        trace = []
+        ts = m.generate(torch.from_numpy(short).to(dt), return_timestamps=True, language="zh", task="transcribe",
+                        max_new_tokens=48, _trace=trace).cpu().numpy()
+        # the fixture's rows (one clip per call, -1-padded) and the margins of every decode step, windows in order
+        # [step, clip]: output position p comes from decode step p within the first window's kept tokens (the tokens
+        # its segments keep, retrieve_segment on the engine's first window of that clip)
         want_ts = [[int(t) for t in r if t != -1] for r in g["f16_ts_ids"]]
         got_ts = [list(map(int, r)) for r in ts]
-        _prefix_equal(got_ts, want_ts, g["f16_ts_margin"].T, TIE, "fp16 timestamps")
+        kept = []
+        for r in range(len(want_ts)):
+            w0 = [t["raw"] for t in trace if t["b"] == r and t["seek"] == 0][0]
+            seq = w0[:-1] if w0 and w0[-1] == EOT else w0
+            kept.append(sum(len(x) for x in retrieve_segment(seq, 3000)[0]))
+        _prefix_equal([x[:k] for x, k in zip(got_ts, kept)], [x[:k] for x, k in zip(want_ts, kept)],
+                      g["f16_ts_margin"].T, TIE, "fp16 timestamps (first windows)")

@@ -277,22 +277,49 @@ def test_fp16_greedy_timestamps_longform_match_hf():
 
 
 def test_lv2_fixture_is_input_sensitive():
-    """the large-v2 decode fixture must show input-dependent decoding, or bit-exact parity on it
-    proves little.  Every greedy row has >= 12 distinct tokens in 48 steps and the rows of an arithmetic >= 15 on
-    average (the fixture: 17-21 per fp32 row, 13-21 fp16, 16-20 bf16), different clips decode to different sequences
-    (greedy and timestamps, in every arithmetic), and the long-form windows decode differently."""
+    """the large-v2 decode fixture must show input-dependent decoding at a moderate
+    dynamic range, or parity on it proves little.  Every greedy row has >= 15 distinct tokens in 48 steps (fixture:
+    35-41), different clips decode to different sequences (greedy and timestamps, in every arithmetic), the long-form
+    windows decode differently; the teacher-forced logits stay within |22.3| (residual stream and logits of
+    moderate range) and HF's own fp16 / bf16 logits agree with its fp32 ones at >= 85 % of the argmaxes (the
+    fixture is not chaotic: fp16 96.9 %, bf16 88.5 %)."""
     g = load_golden("lv2_decode")
     for tag in ("f32", "f16", "b16"):
         ids = g[f"{tag}_greedy_ids"]
         assert ids.shape[0] == 4
         nd = [len(set(r.tolist())) for r in ids]
-        assert min(nd) >= 12 and sum(nd) >= 15 * len(nd), (tag, nd)
+        assert min(nd) >= 15, (tag, nd)
         rows = [tuple(r.tolist()) for r in ids]
         assert len(set(rows)) == len(rows), tag
         ts = [tuple(t for t in r.tolist() if t != -1) for r in g[f"{tag}_ts_ids"]]
         assert len(set(ts)) == len(ts), (tag, ts)
         assert g[f"{tag}_greedy_margin"].shape == (48, 4)
+        # no timestamp token in the no-timestamp greedy rows (suppressed: LV2_GREEDY_SUPPRESS)
+        assert (ids < 50364).all(), tag
     lo = g["f32_long_ids"][0].tolist()
     nw = len(g["f32_long_window_steps"])
     assert nw >= 2 and len(set(lo)) >= 15 and len(g["f32_long_avg_logprobs"]) == nw
     assert len(set(np.round(g["f32_long_avg_logprobs"], 6).tolist())) == nw        # every window decodes differently
+    assert np.abs(g["tf_f32_vals"]).max() < 30.0
+    valid = np.arange(48)[None, :] < g["tf_len"][:, None]
+    for tag in ("f16", "b16"):
+        assert (g["tf_f32_argmax"][valid] == g[f"tf_{tag}_argmax"][valid]).mean() >= 0.85, tag
+    assert g["v_bias"].shape == (32, 1280) and np.isfinite(g["v_bias"]).all()
+
+
+def test_batched_longform_fixture():
+    """The batched long-form fixture (make_golden.py gen_batched_longform): one HF call on 3 recordings keeps them in
+    one batch -- the first seek iteration decodes all three first windows, recordings leave the batch as their seek
+    passes their length, and each recording's windows advance its seek."""
+    g = load_golden("batched_longform")
+    for dims in ("micro", "lv2"):
+        k = f"bl_{dims}"
+        if f"{k}_ids" not in g:
+            continue
+        b, seek = g[f"{k}_win_b"].tolist(), g[f"{k}_win_seek"].tolist()
+        assert b[:3] == [0, 1, 2] and seek[:3] == [0, 0, 0], (b, seek)
+        lens = [6500, 4130, 1820]
+        for r in range(3):
+            sk = [s_ for b_, s_ in zip(b, seek) if b_ == r]
+            assert sk == sorted(sk) and all(s_ < lens[r] for s_ in sk), (r, sk)
+        assert g[f"{k}_ids"].shape[0] == 3 and len(g[f"{k}_win_avg"]) == len(b) == len(g[f"{k}_win_ns"])
