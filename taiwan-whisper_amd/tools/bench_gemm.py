@@ -8,21 +8,24 @@ import torch
 
 from tw import ops
 
-VARIANTS = (("t128", 256), ("t256", 512), ("s3", 1024), ("pp", 2048))
+VARIANTS = (("dflt", 0), ("t128", 256), ("t256", 512), ("s3", 1024), ("pp", 2048))   # dflt: the library's own pick
 SHAPES = [  # (name, M, N, K, a_trans, b_trans)
     ("enc qkv", 96000, 3840, 1280, 0, 0), ("enc out", 96000, 1280, 1280, 0, 0),
     ("enc fc1", 96000, 5120, 1280, 0, 0), ("enc fc2", 96000, 1280, 5120, 0, 0),
     ("xattn kv", 96000, 2560, 1280, 0, 0), ("dec fc1", 28608, 5120, 1280, 0, 0),
     ("dec out", 28608, 1280, 1280, 0, 0), ("lm head", 28608, 51904, 1280, 0, 0),
+    ("dec qkv", 28608, 3840, 1280, 0, 0), ("dec fc2", 28608, 1280, 5120, 0, 0),
     ("dW fc1", 5120, 1280, 28608, 1, 1), ("dX fc2", 28608, 5120, 1280, 0, 1),
     ("dW head", 51904, 1280, 28608, 1, 1), ("dX head", 28608, 1280, 51904, 0, 1),
 ]
 
 
-def main(rounds=5):
+def main(rounds=5, only=None):
     dev = "cuda"
     res = {}
     for name, M, N, K, at, bt in SHAPES:
+        if only and not any(o in name for o in only):
+            continue
         A = (torch.randn(K, M, device=dev) if at else torch.randn(M, K, device=dev)).to(torch.bfloat16)
         B = (torch.randn(K, N, device=dev) if bt else torch.randn(N, K, device=dev)).to(torch.bfloat16)
         C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
@@ -50,4 +53,4 @@ def main(rounds=5):
 
 
 if __name__ == "__main__":
-    main()
+    main(only=sys.argv[1].split(",") if len(sys.argv) > 1 else None)

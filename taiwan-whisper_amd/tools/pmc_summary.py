@@ -43,8 +43,9 @@ def load(d, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    tag = sys.argv[4] if len(sys.argv) > 4 else "latest"
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
-    res = {}
+    res = {"source": f"bash taiwan-whisper_amd/tools/profile_round.sh {tag} (profiles/{tag}_pmc.json)"}
     for fam in FAMILIES:
         if not fetch.get(fam) or not write.get(fam):
             continue

@@ -17,7 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fet
 echo "fetch pass done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $BENCH > $OUT/pmc_write.log 2>&1
 echo "write pass done"
-python3 $R/taiwan-whisper_amd/tools/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_$TAG.json
+python3 $R/taiwan-whisper_amd/tools/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_$TAG.json $TAG
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1
 echo "trace pass done"
 cd $R
