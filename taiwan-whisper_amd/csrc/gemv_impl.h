@@ -194,8 +194,18 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
         }
       }
     } else {
+      // up to 5 pieces per lane loaded before any is stored: one memory round trip per 2560 columns instead of one
+      // per piece (the rows were just written by the previous launch and come from L2)
       const bf16* xr = p.A + (int64_t)row * p.lda;
-      for (int e = lane * 8; e < K; e += 512) *(bf16x8*)(dst + e) = *(const bf16x8*)(xr + e);
+      for (int e0 = lane * 8; e0 < K; e0 += 5 * 512) {
+        bf16x8 t[5];
+#pragma unroll
+        for (int c = 0; c < 5; ++c)
+          if (e0 + c * 512 < K) t[c] = *(const bf16x8*)(xr + e0 + c * 512);
+#pragma unroll
+        for (int c = 0; c < 5; ++c)
+          if (e0 + c * 512 < K) *(bf16x8*)(dst + e0 + c * 512) = t[c];
+      }
     }
   }
 }
@@ -218,6 +228,58 @@ __device__ __forceinline__ void fma8(float& acc, const bf16x8& w, const bf16x8& 
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc = fmaf(e2f<H>(w[q]), e2f<H>(a[q]), acc);
+  }
+}
+
+// NV values per lane -> lane l returns the wave total of value `idx` (idx = -1: this lane holds none).  Stage xor 32:
+// v_permlane32_swap(vdst = y, vsrc = x) leaves lanes 0..31 y_l + y_(l+32) and lanes 32..63 x_(l-32) + x_l -- the
+// operands of swap32_sum in the same order -- so pairing value j with j + NV/2 halves the values per lane; stage
+// xor 16 does the same within each 32-lane half (v_permlane16_swap: even 16-lane rows keep the second value of a
+// pair); the rest (xor 8, 4, 2, 1) run on the remaining values as in wave_sum_dpp.
+template <int NV>
+__device__ __forceinline__ float wave_reduce_scatter(const float (&v)[NV], int lane, int& idx) {
+  const bool hiA = lane >= 32, hiB = (lane & 16) != 0;
+  if constexpr (NV == 1) {
+    idx = lane == 0 ? 0 : -1;
+    return wave_sum_dpp(v[0]);
+  } else {
+    constexpr int NA = NV / 2;
+    float w[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j + NA]), __float_as_uint(v[j]), false, false);
+      w[j] = __uint_as_float(a[0]) + __uint_as_float(a[1]);      // lanes < 32: value j + NA; lanes >= 32: value j
+    }
+    if constexpr (NA == 1) {
+      float t = swap16_sum(w[0]);
+      t += TW_DPP(t, TW_ROW_ROR(8));
+      t += TW_DPP(t, TW_ROW_ROR(4));
+      t += TW_DPP(t, TW_ROW_ROR(2));
+      t += TW_DPP(t, TW_ROW_ROR(1));
+      idx = (lane & 31) == 0 ? (hiA ? 0 : 1) : -1;
+      return t;
+    } else {
+      constexpr int NB = NA / 2;
+      float u[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[j + NB]), __float_as_uint(w[j]), false, false);
+        u[j] = __uint_as_float(a[0]) + __uint_as_float(a[1]);    // even rows: w[j + NB]; odd rows: w[j]
+      }
+      float mine = 0.f;
+      const int jl = lane & 15;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        float t = u[j];
+        t += TW_DPP(t, TW_ROW_ROR(8));
+        t += TW_DPP(t, TW_ROW_ROR(4));
+        t += TW_DPP(t, TW_ROW_ROR(2));
+        t += TW_DPP(t, TW_ROW_ROR(1));
+        if (jl == j) mine = t;
+      }
+      idx = jl < NB ? jl + (hiB ? 0 : NB) + (hiA ? 0 : NA) : -1;
+      return mine;
+    }
   }
 }
 
@@ -255,20 +317,21 @@ __device__ __forceinline__ void gemv_finish(const GemmP& p, const GemvKV& kv, co
       }
     }
   }
-  // every lane gets every (column, row) total; lane c * MR + r then runs the epilogue of (n0 + c, r), all outputs of
-  // the wave at once (the same per-element arithmetic as a single lane running them in turn)
-  float mine = 0.f;
+  // the wave's CPW x MR totals, each the xor 32, 16, 8, 4, 2, 1 butterfly of wave_sum_dpp (the same additions in the
+  // same order: bit-identical to summing each value alone), as a reduce-scatter: a v_permlane32/16_swap exchanges two
+  // values at once, so the first two stages move half, then a quarter of the values; one lane per value then runs
+  // its epilogue (the same per-element arithmetic as a single lane running them in turn)
+  static_assert(CPW * MR <= 64, "one output per lane");
+  float vals[CPW * MR];
 #pragma unroll
   for (int c = 0; c < CPW; ++c)
 #pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      const float tot = wave_sum_dpp(acc[c][r]);
-      if (lane == c * MR + r) mine = tot;
-    }
-  static_assert(CPW * MR <= 64, "one output per lane");
-  const int c = lane / MR, r = lane % MR;
+    for (int r = 0; r < MR; ++r) vals[c * MR + r] = acc[c][r];
+  int idx;
+  const float mine = wave_reduce_scatter<CPW * MR>(vals, lane, idx);
+  const int c = idx / MR, r = idx % MR;
   const int n = n0 + c;
-  if (c < CPW && r < p.M && n < p.N) {
+  if (idx >= 0 && r < p.M && n < p.N) {
     const float v = epi_value<H>(p, r, n, mine);
     const int64_t co = (int64_t)r * p.ldc + n;
     if (p.c_dtype == TW_BF16) ((bf16*)p.C)[co] = f2e<H>(v);
