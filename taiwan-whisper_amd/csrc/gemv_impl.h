@@ -97,10 +97,10 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
           for (int q = 0; q < 8; ++q) s[j] += e2f<H>(t[j][c][q]);
     }
+    // xor 16, 8, 4, 2, 1 within each 32-lane half on permlane / DPP (half_sum_dpp: the order of the __shfl_xor
+    // butterfly it replaces, bit-identical, without the ds_bpermute round trips)
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1)
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) s[j] += __shfl_xor(s[j], o, 64);
+    for (int j = 0; j < RPW; ++j) s[j] = half_sum_dpp(s[j]);
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       mean[j] = s[j] / K;
@@ -111,10 +111,10 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
           for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[j][c][q]) - mean[j]; s[j] += d * d; }
     }
+    // xor 16, 8, 4, 2, 1 within each 32-lane half on permlane / DPP (half_sum_dpp: the order of the __shfl_xor
+    // butterfly it replaces, bit-identical, without the ds_bpermute round trips)
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1)
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) s[j] += __shfl_xor(s[j], o, 64);
+    for (int j = 0; j < RPW; ++j) s[j] = half_sum_dpp(s[j]);
 #pragma unroll
     for (int j = 0; j < RPW; ++j) rstd[j] = rsqrtf(s[j] / K + eps);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of the LN parameters have landed
@@ -163,8 +163,7 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
         for (int q = 0; q < 8; ++q) s += e2f<H>(t[q]);
       }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      s = half_sum_dpp(s);
       const float mean = s / K;
       float ss = 0.f;
       for (int c = 0; c < nch; ++c) {
@@ -172,8 +171,7 @@ __device__ __forceinline__ void gemv_stage_rows(const GemmP& p, const float* __r
 #pragma unroll
         for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[q]) - mean; ss += d * d; }
       }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      ss = half_sum_dpp(ss);
       const float rstd = rsqrtf(ss / K + eps);
       if (lane < 32) {
         for (int c = 0; c < nch; ++c) {

@@ -140,16 +140,14 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16* __restrict
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += e2f<H>(t[c][q]);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  s = half_sum_dpp(s);          // xor 16, 8, 4, 2, 1: the __shfl_xor butterfly's order on permlane / DPP
   const float mean = s / D;
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int q = 0; q < 8; ++q) { const float d = e2f<H>(t[c][q]) - mean; ss += d * d; }
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  ss = half_sum_dpp(ss);
   const float rstd = rsqrtf(ss / D + eps);
   __syncthreads();
   if (!ok) return;
