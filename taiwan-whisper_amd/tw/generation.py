@@ -674,8 +674,11 @@ def need_fallback(tokens, avg_logprob, no_speech_prob, vocab_size, compression_r
 
 
 def _bucket(n):
-    """Decode-batch size for n rows: the next power of two (the extra rows repeat the first one and are dropped), so
-    that a shrinking batch -- recordings finishing, fewer rows falling back -- reuses a captured step."""
+    """Decode-batch size for n rows: the next power of two up to 8 (the GEMV regime: one launch per Linear whatever the
+    rows), then the next multiple of 8; the extra rows repeat the first one and are dropped.  A shrinking batch --
+    recordings finishing, fewer rows falling back -- then reuses a captured step."""
+    if n > 8:
+        return (n + 7) // 8 * 8
     b = 1
     while b < n:
         b *= 2

@@ -114,6 +114,36 @@ def test_batched_recordings_stay_together(monkeypatch):
     assert out[0].tolist() == solo0
 
 
+def test_batched_recordings_empty_and_level_by_level(monkeypatch):
+    """A recording of length 0 never enters the batch (HF: seek >= max_frames from the start) and comes back as an
+    all-pad row; fallback_batch=False decodes the failing rows level by level (one temperature per decode), with the
+    same tokens as the speculative form."""
+    monkeypatch.setattr(generation, "_Decoder", _ScriptedDecoder)
+    script = _script()
+    script[(2, 0.0)] = [TS0, 500, 501, TS0 + 20, EOS]
+    feats = torch.zeros(3, 80, 6000)
+    feats[0, :, 3000:] = 1.0
+    feats[2] = 2.0
+    mask = torch.ones(3, 6000, dtype=torch.long)
+    mask[1] = 0                                                    # recording 1: empty
+    mask[2, 2500:] = 0
+    gc = GenerationConfig(decoder_start_token_id=50258, eos_token_id=EOS, pad_token_id=EOS,
+                          no_timestamps_token_id=50363, suppress_tokens=[], lang_to_id={"<|zh|>": 50260})
+    outs = []
+    for fb in (True, False):
+        _ScriptedDecoder.script = script
+        trace = []
+        out = generation._longform(_model(), gc, feats, mask, "zh", "transcribe", None, 40, False, 3000, trace,
+                                   temperature=(0.0, 0.2, 0.4, 0.6), compression_ratio_threshold=1.35,
+                                   fallback_batch=fb)
+        assert 1 not in {t["b"] for t in trace}
+        assert set(out[1].tolist()) == {EOS}
+        if not fb:
+            assert all(t["batch"] <= 2 for t in trace)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_row_tokens():
     assert generation.row_tokens([1, 2, EOS, EOS, EOS], EOS) == [1, 2, EOS]
     assert generation.row_tokens([1, 2, 3], EOS) == [1, 2, 3]
