@@ -755,11 +755,16 @@ int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
   if ((p.N & 3) || (p.ldc & 3) || ((uintptr_t)p.C & 15)) return 0;
   const int64_t tiles = (int64_t)((p.M + 127) / 128) * ((p.N + 127) / 128);
   if (tiles >= 512) return 0;
+  // the smallest S filling 512 workgroups; where none does (few tiles, or K too short for 16 chunks), the largest S
+  // that still leaves >= 512 k per chunk (round 6: c2's decoder 768 x 768 weight gradients at K = 14 304 tokens ran
+  // unsplit on 36 workgroups, 226 us each, 36 per step; the conv-stem weight gradient on 12)
+  int best = 0;
   for (int S = 2; S <= 16; S *= 2) {
-    if (p.K % S != 0 || p.K / S < 1024) break;      // chunk tails are masked like any K tail
-    if (tiles * S >= 512) return S;
+    if (p.K % S != 0 || p.K / S < 512) break;
+    best = S;
+    if (tiles * S >= 512) break;
   }
-  return 0;
+  return best;
 }
 
 template <bool H, bool AT, bool BT>
@@ -959,7 +964,7 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (!a_trans && !b_trans && K >= 8192 && t256 >= pp_grid_cus()) tile = 256;
   // ... and its transposed-B form (the student's LM-head dX = dlogits . E, K = 51 904, 560 tiles) on the 2-stage
   // 256x256 tile: 4059 vs 4370 us on the 128x128 one (tools/bench_gemm.py "dX head", profiles/r06_a_gemm.log)
-  if (!a_trans && b_trans && K >= 8192 && t256 >= pp_grid_cus()) tile = 256;
+  if (!a_trans && b_trans && K >= 8192 && t256 >= pp_grid_cus() / 2) tile = 256;   // c2's: 168 tiles, 1297 vs 1643 us
   // K-major forward grids of 1-4 rounds whose rounds are well filled (c2's B = 32 shapes: the teacher encoder's
   // N = 1280 Linears at M = 48 000, 940 256-tiles = 3.67 rounds, 92 % of the workgroup-rounds busy; the student
   // decoder's fused QKV and fc1): the persistent kernel.  Grids with a mostly idle last round take the whole-round

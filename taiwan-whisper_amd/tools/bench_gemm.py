@@ -20,11 +20,26 @@ SHAPES = [  # (name, M, N, K, a_trans, b_trans)
 ]
 
 
+# config 2 (whisper-small student d = 768 at B = 32: encoder rows 48 000, decoder rows 14 304; trainable encoder):
+# forward and the backward dX (W transposed) / dW (both transposed, K = tokens) products
+SHAPES_C2 = [
+    ("s enc qkv", 48000, 2304, 768, 0, 0), ("s enc out", 48000, 768, 768, 0, 0), ("s enc fc1", 48000, 3072, 768, 0, 0),
+    ("s enc fc2", 48000, 768, 3072, 0, 0), ("s dec qkv", 14304, 2304, 768, 0, 0), ("s lm head", 14304, 51904, 768, 0, 0),
+    ("s dX fc1", 48000, 768, 3072, 0, 1), ("s dX fc2", 48000, 3072, 768, 0, 1), ("s dX qkv", 48000, 768, 2304, 0, 1),
+    ("s dW fc1", 3072, 768, 48000, 1, 1), ("s dW fc2", 768, 3072, 48000, 1, 1), ("s dW qkv", 2304, 768, 48000, 1, 1),
+    ("s dW out", 768, 768, 48000, 1, 1), ("s dX head", 14304, 768, 51904, 0, 1), ("s dW head", 51904, 768, 14304, 1, 1),
+    ("s dec out", 14304, 768, 768, 0, 0), ("s dec fc2", 14304, 768, 3072, 0, 0), ("s dec fc1", 14304, 3072, 768, 0, 0),
+    ("s dX decfc1", 14304, 768, 3072, 0, 1), ("s xkv", 48000, 1536, 768, 0, 0),
+    ("t enc out", 48000, 1280, 1280, 0, 0), ("t enc fc1", 48000, 5120, 1280, 0, 0), ("t dec out", 14304, 1280, 1280, 0, 0),
+]
+
+
 def main(rounds=5, only=None):
     dev = "cuda"
     res = {}
-    for name, M, N, K, at, bt in SHAPES:
-        if only and not any(o in name for o in only):
+    shapes = SHAPES_C2 if only == ["c2"] else SHAPES
+    for name, M, N, K, at, bt in shapes:
+        if only and only != ["c2"] and not any(o in name for o in only):
             continue
         A = (torch.randn(K, M, device=dev) if at else torch.randn(M, K, device=dev)).to(torch.bfloat16)
         B = (torch.randn(K, N, device=dev) if bt else torch.randn(N, K, device=dev)).to(torch.bfloat16)
