@@ -969,7 +969,9 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   // N = 1280 Linears at M = 48 000, 940 256-tiles = 3.67 rounds, 92 % of the workgroup-rounds busy; the student
   // decoder's fused QKV and fc1): the persistent kernel.  Grids with a mostly idle last round take the whole-round
   // + 128x128 tail split below (dp_tail_plan).  Fill threshold 85 % (c2 +0.6 %, c3 unchanged: same box, round 4)
-  if (!a_trans && !b_trans && tile == 128 && K >= 256) {
+  // (K >= 1024: at c2's student decoder K = 768 -- 12 K-tiles per tile -- the 128x128 kernel wins: fused QKV 69 vs
+  // 85 us, fc1 90 vs 105 us, profiles/r06_l_gemm_c2.log)
+  if (!a_trans && !b_trans && tile == 128 && K >= 1024) {
     const int64_t G = pp_grid_cus();
     if (t256 >= G && t256 * 100 >= ((t256 + G - 1) / G) * G * 85) tile = 256;
   }
