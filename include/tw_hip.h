@@ -123,7 +123,8 @@ int tw_transpose_bf16(const void* src, int64_t ld_src, int rows, int cols, void*
                       tw_stream_t stream);
 /* autocast weight cast fp32 -> bf16 (ACC:accelerator.py autocast of every Linear weight). */
 int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, tw_stream_t stream);
-/* bias gradient: out[c] (+)= [bf16](sum_r x[r][c]); deterministic two-pass, workspace >= ceil(rows/256)*cols. */
+/* bias gradient: out[c] (+)= [round](sum_r x[r][c]) (round_bf16: 0 none, 1 to bf16, 2 to fp16; x fp32 / bf16 / fp16);
+ * deterministic two-pass, workspace >= ceil(rows/256)*cols. */
 int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum, int round_bf16,
               float* workspace, int64_t workspace_floats, tw_stream_t stream);
 
@@ -252,13 +253,21 @@ int tw_gelu_bwd_f32(const float* g, const float* pre, float* out, int64_t n, tw_
  * decode call sites (training/run_eval.py:99 `--dtype float16` default, :500-509 `model.to(dtype)`, :589
  * `input_features.to(dtype)`; training/run_pseudo_labelling.py:461-463 under run-pseudo-labelling.sh:30):
  * v_mfma_f32_16x16x32_f16 with fp32 accumulation, every 16-bit operand / output IEEE fp16 (RNE).
- * tw_gemm_f16: tw_gemm_bf16 for fp16 operands, forward products only (a_trans = b_trans = 0; else 2);
+ * tw_gemm_f16: tw_gemm_bf16 for fp16 operands (the decode path uses the forward products only);
  *   A, B, bias, aux fp16; C and res fp16 (code 2) or fp32; epilogue order as tw_gemm_bf16 with the rounding
  *   to fp16, plus TW_GEMM_CLAMP16: after the residual add, clamp to +-(65504 - 1000) (HF WhisperEncoderLayer,
  *   modeling_whisper.py:409-411, the fp16 encoder stream).
  * tw_gemv_f16: tw_gemv_bf16 for fp16 x / W / bias / C (LayerNorm fused as there, fp16 output of the LN).
  * tw_attn_fwd_f16: tw_attn_fwd for fp16 Q/K/V/O (P rounded to fp16 for the PV product, fp32 row sums).
  * tw_mel_to_conv_input_f16: log-mel [B][80][T] fp32 -> fp16 conv1 input [B][T+2][80] (the .to(float16) cast).
+ * fp16-AUTOCAST TRAINING (run_distillation.py:815-817 --dtype float16: mixed_precision="fp16", fp16 teacher,
+ * GradScaler; round 6) uses the same entries plus:
+ *   tw_gemm_f16 with a_trans / b_trans (the dX and dW products; split-K dW rounds its fp32 chunk sum to fp16);
+ *   tw_attn_bwd_f16: tw_attn_bwd for fp16 tensors; tw_gelu_bwd_f16: tw_gelu_bwd for an fp16 activation;
+ *   tw_cast_f32_f16: autocast's fp32 -> fp16 weight cast; tw_colsum with round_bf16 = 2;
+ *   tw_adamw_ex: tw_adamw with the 16-bit weight copy in p16_dtype (1 bf16, 2 fp16) and GradScaler.unscale_
+ *   folded in: g and norm are the loss-scaled gradient and its norm, inv_scale = 1 / scale (a power of two,
+ *   so g * inv_scale is exact); tw_adamw(...) == tw_adamw_ex(..., TW bf16, ..., inv_scale = 1).
  * The dtype-coded entries above (tw_layernorm_fwd, tw_embed_fwd / tw_embed_step, tw_decode_attn, the selection
  * kernels, tw_token_logprob, tw_kv_append, tw_kv_head_major, tw_kl_ce) take code 2 for fp16 rows. */
 #define TW_GEMM_CLAMP16 128
@@ -274,6 +283,15 @@ int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_t ldk, cons
                     int64_t ldo, float* lse, int B, int H, int Tq, int Tk, int head_dim, int causal, float scale,
                     tw_stream_t stream);
 int tw_mel_to_conv_input_f16(const float* mel, void* xt, int B, int nmel, int T, tw_stream_t stream);
+int tw_attn_bwd_f16(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv, const void* O,
+                    int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ, int64_t lddq, void* dK,
+                    int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq, int Tk, int head_dim, int causal,
+                    float scale, float* workspace, tw_stream_t stream);
+int tw_gelu_bwd_f16(const void* g, int g_dtype, const void* pre, void* out, int64_t n, tw_stream_t stream);
+int tw_cast_f32_f16(const float* src, void* dst, int64_t n, tw_stream_t stream);
+int tw_adamw_ex(float* p, const float* g, float* m, float* v, void* p16, int p16_dtype, int64_t n, float lr, float b1,
+                float b2, float eps, float wd, int step, const float* norm, float max_norm, float inv_scale,
+                tw_stream_t stream);
 
 /* ---- host code: FLAC decoding for the data feed (replaces soundfile / libsndfile's sf.read of the
  * reference corpus, dataset/cool_dataset.py:55).  `data` is the whole file in host memory.

@@ -73,17 +73,12 @@ __device__ __forceinline__ bf16x8 ld_frag(const bf16* base, int64_t ld, int row,
   return *(const bf16x8*)(base + (int64_t)row * ld + kk * 32 + 8 * (lane >> 4));
 }
 
-__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
-  return bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
-}
 // P as the 16-bit operand type of the instantiation (bf16 words, or fp16 words for the fp16 path)
 template <bool H>
 __device__ __forceinline__ bf16x8 pack8e(const f32x4& a, const f32x4& b) {
   return bf16x8{f2e<H>(a[0]), f2e<H>(a[1]), f2e<H>(a[2]), f2e<H>(a[3]),
                 f2e<H>(b[0]), f2e<H>(b[1]), f2e<H>(b[2]), f2e<H>(b[3])};
 }
-
-#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 struct AttnP {
   const bf16* Q; const bf16* K; const bf16* V; bf16* O; float* lse;
@@ -298,6 +293,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
 
 // ------------------------------------------------------------------------------------
 // D[b,h,q] = sum_e dO[q][e] * O[q][e]     (one wave per (row, head))
+template <bool F16>
 __global__ void attn_bwd_pre_kernel(const bf16* __restrict__ dO, int64_t lddo, const bf16* __restrict__ O,
                                     int64_t ldo, float* __restrict__ Dv, int B, int H, int Tq) {
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -305,7 +301,7 @@ __global__ void attn_bwd_pre_kernel(const bf16* __restrict__ dO, int64_t lddo, c
   const int lane = lane_id();
   const int h = w % H;
   const int64_t row = w / H;   // b*Tq + q
-  const float v = bf2f(dO[row * lddo + h * 64 + lane]) * bf2f(O[row * ldo + h * 64 + lane]);
+  const float v = e2f<F16>(dO[row * lddo + h * 64 + lane]) * e2f<F16>(O[row * ldo + h * 64 + lane]);
   const float s = wave_sum_dpp(v);
   if (lane == 0) {
     const int b = row / Tq, q = row % Tq;
@@ -314,6 +310,7 @@ __global__ void attn_bwd_pre_kernel(const bf16* __restrict__ dO, int64_t lddo, c
 }
 
 // dQ: per query block, loop over key tiles (K, V in LDS)
+template <bool H>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];
   const int lane = lane_id(), wave = wave_id_uniform();
@@ -375,10 +372,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 kf = rd_row(Ks, kj * 16, kk, lane);
         const bf16x8 vf = rd_row(Vs, kj * 16, kk, lane);
-        s[kj][0] = MFMA(kf, qf[0][kk], s[kj][0]);
-        s[kj][1] = MFMA(kf, qf[1][kk], s[kj][1]);
-        dp[kj][0] = MFMA(vf, dof[0][kk], dp[kj][0]);
-        dp[kj][1] = MFMA(vf, dof[1][kk], dp[kj][1]);
+        s[kj][0] = mma16<H>(kf, qf[0][kk], s[kj][0]);
+        s[kj][1] = mma16<H>(kf, qf[1][kk], s[kj][1]);
+        dp[kj][0] = mma16<H>(vf, dof[0][kk], dp[kj][0]);
+        dp[kj][1] = mma16<H>(vf, dof[1][kk], dp[kj][1]);
       }
     }
     const int k0 = kt * KT;
@@ -401,13 +398,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
     // dQ^T += K^T dS^T
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 d0 = pack8(s[2 * ss][0], s[2 * ss + 1][0]);
-      const bf16x8 d1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
+      const bf16x8 d0 = pack8e<H>(s[2 * ss][0], s[2 * ss + 1][0]);
+      const bf16x8 d1 = pack8e<H>(s[2 * ss][1], s[2 * ss + 1][1]);
 #pragma unroll
       for (int hj = 0; hj < 4; ++hj) {
         const bf16x8 kt_ = rd_tr(Ks, hj * 16, ss, lane);
-        dq[hj][0] = MFMA(kt_, d0, dq[hj][0]);
-        dq[hj][1] = MFMA(kt_, d1, dq[hj][1]);
+        dq[hj][0] = mma16<H>(kt_, d0, dq[hj][0]);
+        dq[hj][1] = mma16<H>(kt_, d1, dq[hj][1]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -421,7 +418,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
 #pragma unroll
       for (int hj = 0; hj < 4; ++hj) {
         const f32x4 v = dq[hj][qi] * p.scale;
-        *(bf16x4*)(out + hj * 16 + 4 * g) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        *(bf16x4*)(out + hj * 16 + 4 * g) = bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
       }
     }
   }
@@ -431,6 +428,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
 // Two workgroups per CU (round 4): 218 VGPRs, two waves per SIMD hide each other's LDS / exp / MFMA latencies.  At
 // one workgroup per CU (round 3: 268-276 VGPRs, accumulators shuffled through AGPRs) the encoder-shape backward
 // took 6.1 ms against 4.6 ms now (tools/bench_attn.py, same box, profiles/r04_h_attn_bwd_ab.log).
+template <bool H>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB + 2 * 2 * 64 * 4];
   const int lane = lane_id(), wave = wave_id_uniform();
@@ -499,10 +497,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnP p) {
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 qa = rd_row(Qs, qf * 16, kk, lane);
         const bf16x8 da = rd_row(dOs, qf * 16, kk, lane);
-        s[qf][0] = MFMA(qa, kf[0][kk], s[qf][0]);
-        s[qf][1] = MFMA(qa, kf[1][kk], s[qf][1]);
-        dp[qf][0] = MFMA(da, vf[0][kk], dp[qf][0]);
-        dp[qf][1] = MFMA(da, vf[1][kk], dp[qf][1]);
+        s[qf][0] = mma16<H>(qa, kf[0][kk], s[qf][0]);
+        s[qf][1] = mma16<H>(qa, kf[1][kk], s[qf][1]);
+        dp[qf][0] = mma16<H>(da, vf[0][kk], dp[qf][0]);
+        dp[qf][1] = mma16<H>(da, vf[1][kk], dp[qf][1]);
       }
     }
     // interior tiles (no query tail, no key tail, not on the causal diagonal: wave-uniform) skip the mask
@@ -526,18 +524,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnP p) {
     // dV^T += dO^T P ; dK^T += Q^T dS
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 p0 = pack8(s[2 * ss][0], s[2 * ss + 1][0]);
-      const bf16x8 p1 = pack8(s[2 * ss][1], s[2 * ss + 1][1]);
-      const bf16x8 d0 = pack8(dp[2 * ss][0], dp[2 * ss + 1][0]);
-      const bf16x8 d1 = pack8(dp[2 * ss][1], dp[2 * ss + 1][1]);
+      const bf16x8 p0 = pack8e<H>(s[2 * ss][0], s[2 * ss + 1][0]);
+      const bf16x8 p1 = pack8e<H>(s[2 * ss][1], s[2 * ss + 1][1]);
+      const bf16x8 d0 = pack8e<H>(dp[2 * ss][0], dp[2 * ss + 1][0]);
+      const bf16x8 d1 = pack8e<H>(dp[2 * ss][1], dp[2 * ss + 1][1]);
 #pragma unroll
       for (int hj = 0; hj < 4; ++hj) {
         const bf16x8 dot = rd_tr(dOs, hj * 16, ss, lane);
         const bf16x8 qt_ = rd_tr(Qs, hj * 16, ss, lane);
-        dv[hj][0] = MFMA(dot, p0, dv[hj][0]);
-        dv[hj][1] = MFMA(dot, p1, dv[hj][1]);
-        dk[hj][0] = MFMA(qt_, d0, dk[hj][0]);
-        dk[hj][1] = MFMA(qt_, d1, dk[hj][1]);
+        dv[hj][0] = mma16<H>(dot, p0, dv[hj][0]);
+        dv[hj][1] = mma16<H>(dot, p1, dv[hj][1]);
+        dk[hj][0] = mma16<H>(qt_, d0, dk[hj][0]);
+        dk[hj][1] = mma16<H>(qt_, d1, dk[hj][1]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -553,8 +551,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnP p) {
       for (int hj = 0; hj < 4; ++hj) {
         const f32x4 a = dk[hj][kj] * p.scale;
         const f32x4 c = dv[hj][kj];
-        *(bf16x4*)(ok_ + hj * 16 + 4 * g) = bf16x4{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3])};
-        *(bf16x4*)(ov_ + hj * 16 + 4 * g) = bf16x4{f2bf(c[0]), f2bf(c[1]), f2bf(c[2]), f2bf(c[3])};
+        *(bf16x4*)(ok_ + hj * 16 + 4 * g) = bf16x4{f2e<H>(a[0]), f2e<H>(a[1]), f2e<H>(a[2]), f2e<H>(a[3])};
+        *(bf16x4*)(ov_ + hj * 16 + 4 * g) = bf16x4{f2e<H>(c[0]), f2e<H>(c[1]), f2e<H>(c[2]), f2e<H>(c[3])};
       }
     }
   }
@@ -603,11 +601,12 @@ extern "C" int tw_attn_fwd_f16(const void* Q, int64_t ldq, const void* K, int64_
   return TW_OK;
 }
 
-// workspace: B*H*Tq floats (the D = rowsum(dO*O) vector)
-extern "C" int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
-                           const void* O, int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ,
-                           int64_t lddq, void* dK, int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq, int Tk,
-                           int head_dim, int causal, float scale, float* workspace, hipStream_t stream) {
+namespace {
+// workspace: B*H*Tq floats (the D = rowsum(dO*O) vector); half: fp16 words (fp16-autocast training), else bf16
+int attn_bwd_run(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv, const void* O,
+                 int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ, int64_t lddq, void* dK,
+                 int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq, int Tk, int head_dim, int causal,
+                 float scale, float* workspace, bool half, hipStream_t stream) {
   if (head_dim != 64) return TW_EUNSUPPORTED;
   if (B <= 0 || Tq <= 0 || Tk <= 0) return TW_OK;
   if (!check_common(Q, K, V, ldq, ldk, ldv) || ((uintptr_t)dO & 15) || (lddo & 7)) return TW_EINVAL;
@@ -619,10 +618,36 @@ extern "C" int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ld
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
   const int64_t nw = (int64_t)B * Tq * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((nw + 3) / 4), dim3(256), 0, stream, (const bf16*)dO, lddo,
-                     (const bf16*)O, ldo, workspace, B, H, Tq);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Tk + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  if (half) {
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<true>, dim3((nw + 3) / 4), dim3(256), 0, stream, (const bf16*)dO, lddo,
+                       (const bf16*)O, ldo, workspace, B, H, Tq);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, dim3((Tk + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<false>, dim3((nw + 3) / 4), dim3(256), 0, stream, (const bf16*)dO, lddo,
+                       (const bf16*)O, ldo, workspace, B, H, Tq);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3((Tk + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
+  }
   TW_CHECK_LAUNCH();
   return TW_OK;
+}
+}  // namespace
+
+extern "C" int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
+                           const void* O, int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ,
+                           int64_t lddq, void* dK, int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq, int Tk,
+                           int head_dim, int causal, float scale, float* workspace, hipStream_t stream) {
+  return attn_bwd_run(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, dQ, lddq, dK, lddk, dV, lddv, B, H, Tq, Tk,
+                      head_dim, causal, scale, workspace, false, stream);
+}
+
+// fp16 Q/K/V/O/dO/dQ/dK/dV (the student's SDPA backward under fp16 autocast, run_distillation.py:815-817
+// mixed_precision="fp16"): the bf16 kernels instantiated for fp16 words (P and dS rounded to fp16 for their MFMAs)
+extern "C" int tw_attn_bwd_f16(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
+                               const void* O, int64_t ldo, const void* dO, int64_t lddo, const float* lse, void* dQ,
+                               int64_t lddq, void* dK, int64_t lddk, void* dV, int64_t lddv, int B, int H, int Tq,
+                               int Tk, int head_dim, int causal, float scale, float* workspace, hipStream_t stream) {
+  return attn_bwd_run(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, dQ, lddq, dK, lddk, dV, lddv, B, H, Tq, Tk,
+                      head_dim, causal, scale, workspace, true, stream);
 }

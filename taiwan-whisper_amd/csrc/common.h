@@ -188,6 +188,16 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float pdf = 0.39894228040143267794f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);
   return cdf + x * pdf;
 }
+// GELU derivative of the instantiation's operand type: bf16 -> the polynomial erf above (its 1.5e-7 absolute error is
+// far below a bf16 ulp of any product); fp16 -> the device erff / expf (torch's gelu backward formula): for x < -3 the
+// polynomial's error is ~1e-4 of gelu'(x), a third of an fp16 ulp, and flips roundings of fp16-autocast gradients
+template <bool H>
+__device__ __forceinline__ float gelu_grad_of(float x) {
+  if constexpr (H)
+    return 0.5f * (1.0f + erff(x * 0.70710678118654752440f)) + x * 0.39894228040143267794f * expf(-0.5f * x * x);
+  else
+    return gelu_erf_grad(x);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -695,8 +695,8 @@ void launch_pp(GemmP p, int batch, hipStream_t stream) {
 // the K range is cut into S chunks run as S batch entries of the 128x128 kernel into an fp32
 // workspace, then one pass sums the chunks in order and applies the epilogue
 //     C = [C +] round?(alpha * sum_s ws[s])
-// (bf16 rounding point of the autocast product as in the unsplit kernel; the fp32 sum over K is
-// regrouped by chunk).  Workspace: splitk_workspace (per device, never freed).
+// (16-bit rounding point of the autocast product as in the unsplit kernel -- round 1: bf16, 2: fp16; the fp32
+// sum over K is regrouped by chunk).  Workspace: splitk_workspace (per device, never freed).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t split_stride,
                                                             float* __restrict__ C, int64_t ldc, int M, int N,
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     float* cp = C + (int64_t)m * ldc + c;
     f32x4 o;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = round ? rbf(alpha * a[r]) : alpha * a[r];
+    for (int r = 0; r < 4; ++r) o[r] = round == 2 ? rnd<true>(alpha * a[r]) : round ? rbf(alpha * a[r]) : alpha * a[r];
     if (accum) o += *(const f32x4*)cp;
     *(f32x4*)cp = o;
   }
@@ -720,6 +720,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // Split-K workspace: one block per device, grown (never freed: a captured HIP graph may hold the
 // pointer of an older block, so old blocks are kept) outside stream capture only.  GEMMs of one
 // device are issued from one stream at a time (the trainer's and the decoder's current stream).
+// (gemm_f16.hip compiles this file again for the fp16 entry points and uses this TU's block)
+#ifdef TW_GEMM_TU_F16
+}  // namespace
+void* tw_device_workspace(hipStream_t stream, size_t bytes);
+namespace {
+void* splitk_workspace(hipStream_t stream, size_t bytes) { return tw_device_workspace(stream, bytes); }
+#else
 void* splitk_workspace(hipStream_t stream, size_t bytes) {
   // at least 4 MiB per allocation: the small users (decode-attention partials, selection partials) then
   // find the block already large enough inside a captured decode step once any eager call has run
@@ -746,6 +753,7 @@ void* splitk_workspace(hipStream_t stream, size_t bytes) {
   cur.push_back({dev, {ptr, bytes}});
   return ptr;
 }
+#endif
 
 // S for a dW-shaped call, 0 = no split: fewer than 512 128x128 tiles, K split into S equal chunks of
 // >= 1024 until >= 512 workgroups; fp32 output, flags within {ROUND, ACCUM}.
@@ -769,6 +777,13 @@ int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
 
 template <bool H, bool AT, bool BT>
 void dispatch(GemmP p, int batch, hipStream_t stream, int tile) {
+  if constexpr (H && (AT || BT)) {
+    // fp16 training's dX / dW products: the 2-stage 256x256 and 128x128 tiles only (the 256x128 rings are forced
+    // A/B variants of the bf16 kernels; not instantiating them for fp16 keeps the library's build time down)
+    if (tile == 256) launch<H, AT, BT, 256, 256, 2, 4, 2>(p, batch, stream);
+    else launch<H, AT, BT, 128, 128, 2, 2, 2>(p, batch, stream);
+    return;
+  }
   if (tile == 2562 && !AT && !BT) launch_pp<H>(p, batch, stream);
   else if (tile == 1284) {
     if constexpr (!AT && !BT) launch<H, AT, BT, 128, 128, 2, 2, 4>(p, batch, stream);   // 4-stage ring
@@ -905,11 +920,14 @@ int launch_dp_tail(const GemmP& p, int m_dp, hipStream_t stream) {
 }  // namespace
 
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
+#ifndef TW_GEMM_TU_F16
 void* tw_device_workspace(hipStream_t stream, size_t bytes) { return splitk_workspace(stream, bytes); }
+#endif
 
 namespace {
 
-// H = false: tw_gemm_bf16; H = true: tw_gemm_f16 (forward products only: K-major A and B)
+// H = false: tw_gemm_bf16; H = true: tw_gemm_f16 (the fp16 model's forward products, and since round 6 the
+// transposed dX / dW products of fp16-autocast training: the same kernels instantiated for fp16 words)
 template <bool H>
 int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans, void* C, int64_t ldc,
              int c_dtype, int M, int N, int K, int batch, int64_t sA, int64_t sB, int64_t sC, float alpha,
@@ -917,7 +935,6 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
              int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return TW_OK;
   if (H) {
-    if (a_trans || b_trans) return TW_EUNSUPPORTED;
     if ((c_dtype != TW_F32 && c_dtype != TW_F16) || ((flags & F_RES) && res_dtype != TW_F32 && res_dtype != TW_F16))
       return TW_EUNSUPPORTED;
     // inside the kernels the 16-bit code means "the operand type" (gemm_impl.h)
@@ -1013,7 +1030,7 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     TW_CHECK_LAUNCH();
     return TW_OK;
   }
-  if (!H && !(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
+  if (!(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
     const int S = splitk_factor(p, batch, a_trans, b_trans);
     const size_t bytes = (size_t)S * M * N * sizeof(float);
     void* ws = (S > 0 && bytes <= ((size_t)1 << 30)) ? splitk_workspace(stream, bytes) : nullptr;
@@ -1026,12 +1043,12 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
       q.C = ws; q.ldc = N; q.sC = (int64_t)M * N; q.c_dtype = TW_F32;
       q.alpha = 1.f; q.flags = 0; q.bias = nullptr; q.res = nullptr; q.aux = nullptr;
       q.epi = pick_epilogue(q, S);
-      launch<false, true, true, 128, 128, 2, 2, 2>(q, S, stream);
+      launch<H, true, true, 128, 128, 2, 2, 2>(q, S, stream);
       TW_CHECK_LAUNCH();
       const int64_t work = (int64_t)M * (N / 4);
       const int grid = (int)std::min<int64_t>((work + 255) / 256, 4096);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, stream, (const float*)ws, S,
-                         (int64_t)M * N, (float*)C, ldc, M, N, alpha, (flags & F_ROUND) ? 1 : 0,
+                         (int64_t)M * N, (float*)C, ldc, M, N, alpha, (flags & F_ROUND) ? (H ? 2 : 1) : 0,
                          (flags & F_ACCUM) ? 1 : 0);
       TW_CHECK_LAUNCH();
       return TW_OK;
@@ -1066,14 +1083,10 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (tile == 128 && !a_trans && !b_trans && !(flags & 256) &&
       (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch <= pp_grid_cus())
     tile = 1284;
-  if constexpr (H) {
-    dispatch<true, false, false>(p, batch, stream, tile);
-  } else {
-    if (!a_trans && !b_trans) dispatch<false, false, false>(p, batch, stream, tile);
-    else if (!a_trans && b_trans) dispatch<false, false, true>(p, batch, stream, tile);
-    else if (a_trans && !b_trans) dispatch<false, true, false>(p, batch, stream, tile);
-    else dispatch<false, true, true>(p, batch, stream, tile);
-  }
+  if (!a_trans && !b_trans) dispatch<H, false, false>(p, batch, stream, tile);
+  else if (!a_trans && b_trans) dispatch<H, false, true>(p, batch, stream, tile);
+  else if (a_trans && !b_trans) dispatch<H, true, false>(p, batch, stream, tile);
+  else dispatch<H, true, true>(p, batch, stream, tile);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
@@ -1146,6 +1159,7 @@ int gemv_run(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, f
 
 }  // namespace
 
+#ifndef TW_GEMM_TU_F16
 extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
                             void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
                             int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
@@ -1153,15 +1167,6 @@ extern "C" int tw_gemm_bf16(const void* A, int64_t lda, int a_trans, const void*
                             void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
   return gemm_run<false>(A, lda, a_trans, B, ldb, b_trans, C, ldc, c_dtype, M, N, K, batch, sA, sB, sC, alpha, bias,
                          res, ldr, sR, res_dtype, res_mod, aux, ldaux, sAux, flags, stream);
-}
-
-extern "C" int tw_gemm_f16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
-                           void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
-                           int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
-                           const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
-                           void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
-  return gemm_run<true>(A, lda, a_trans, B, ldb, b_trans, C, ldc, c_dtype, M, N, K, batch, sA, sB, sC, alpha, bias,
-                        res, ldr, sR, res_dtype, res_mod, aux, ldaux, sAux, flags, stream);
 }
 
 extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
@@ -1173,6 +1178,16 @@ extern "C" int tw_gemv_bf16(const void* x, int64_t ldx, const float* ln_w, const
                          ldaux, flags, kv_cache, kv_sb, kv_ld, kv_col0, t_dev, stream);
 }
 
+#else
+extern "C" int tw_gemm_f16(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb, int b_trans,
+                           void* C, int64_t ldc, int c_dtype, int M, int N, int K, int batch,
+                           int64_t sA, int64_t sB, int64_t sC, float alpha, const void* bias,
+                           const void* res, int64_t ldr, int64_t sR, int res_dtype, int res_mod,
+                           void* aux, int64_t ldaux, int64_t sAux, int flags, hipStream_t stream) {
+  return gemm_run<true>(A, lda, a_trans, B, ldb, b_trans, C, ldc, c_dtype, M, N, K, batch, sA, sB, sC, alpha, bias,
+                        res, ldr, sR, res_dtype, res_mod, aux, ldaux, sAux, flags, stream);
+}
+
 extern "C" int tw_gemv_f16(const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps, const void* W,
                            int64_t ldw, void* C, int64_t ldc, int c_dtype, int M, int N, int K, const void* bias,
                            const void* res, int64_t ldr, int res_dtype, void* aux, int64_t ldaux, int flags,
@@ -1181,3 +1196,4 @@ extern "C" int tw_gemv_f16(const void* x, int64_t ldx, const float* ln_w, const 
   return gemv_run<true>(x, ldx, ln_w, ln_b, eps, W, ldw, C, ldc, c_dtype, M, N, K, bias, res, ldr, res_dtype, aux,
                         ldaux, flags, kv_cache, kv_sb, kv_ld, kv_col0, t_dev, stream);
 }
+#endif

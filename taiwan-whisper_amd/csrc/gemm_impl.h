@@ -203,7 +203,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
         for (int r = 0; r < 4; ++r) {
           v[r] = p.alpha * acc[mi][ni][r] + bv[ni][r];
           if (flags & F_ROUND) v[r] = rnd<H>(v[r]);
-          if (flags & F_DGELU) v[r] = rnd<H>(v[r] * gelu_erf_grad(ex[ni][r]));
+          if (flags & F_DGELU) v[r] = rnd<H>(v[r] * gelu_grad_of<H>(ex[ni][r]));
         }
         if (flags & F_GELU) {
           if (flags & F_AUX_OUT)
@@ -249,7 +249,7 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
       }
       if (flags & F_DGELU) {
         const bf16* ax = p.aux + bz * p.sAux + (int64_t)m * p.ldaux + n;
-        for (int r = 0; r < nv; ++r) v[r] = rnd<H>(v[r] * gelu_erf_grad(e2f<H>(ax[r])));
+        for (int r = 0; r < nv; ++r) v[r] = rnd<H>(v[r] * gelu_grad_of<H>(e2f<H>(ax[r])));
       }
       if (flags & F_GELU) {
         if (flags & F_AUX_OUT) {

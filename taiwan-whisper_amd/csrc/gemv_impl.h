@@ -12,7 +12,7 @@ __device__ __forceinline__ float epi_value(const GemmP& p, int m, int n, float v
   v *= p.alpha;
   if (flags & F_BIAS) v += e2f<H>(p.bias[n]);
   if (flags & F_ROUND) v = rnd<H>(v);
-  if (flags & F_DGELU) v = rnd<H>(v * gelu_erf_grad(e2f<H>(p.aux[(int64_t)m * p.ldaux + n])));
+  if (flags & F_DGELU) v = rnd<H>(v * gelu_grad_of<H>(e2f<H>(p.aux[(int64_t)m * p.ldaux + n])));
   if (flags & F_GELU) {
     if (flags & F_AUX_OUT) p.aux[(int64_t)m * p.ldaux + n] = f2e<H>(v);
     v = rnd<H>(gelu_of<H>(v));

@@ -23,14 +23,16 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const void* __
   }
 }
 
+// H: fp16 words (fp16 autocast's weight cast), else bf16
+template <bool H>
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int64_t n) {
   int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (; i + 3 < n; i += stride) {
     f32x4 v = *(const f32x4*)(src + i);
-    *(bf16x4*)(dst + i) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    *(bf16x4*)(dst + i) = bf16x4{f2e<H>(v[0]), f2e<H>(v[1]), f2e<H>(v[2]), f2e<H>(v[3])};
   }
-  for (; i < n; ++i) dst[i] = f2bf(src[i]);
+  for (; i < n; ++i) dst[i] = f2e<H>(src[i]);
 }
 
 // Column sums over rows (bias gradient of an autocast Linear, computed in bf16 then added to the
@@ -53,6 +55,11 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restr
         const bf16x8 v = *(const bf16x8*)((const bf16*)x + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+      } else if (x_dtype == TW_F16) {
+        float t[8];
+        load8((const f16*)x + o, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += t[j];
       } else {
         const f32x4 a = *(const f32x4*)((const float*)x + o);
         const f32x4 b = *(const f32x4*)((const float*)x + o + 4);
@@ -73,7 +80,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restr
   }
 }
 
-// out[c] = [out[c] +] round?(sum_k partial[k][c]): 64 columns per block, 16 thread rows each
+// out[c] = [out[c] +] round?(sum_k partial[k][c]) (round 1: to bf16, 2: to fp16): 64 columns per block, 16 thread rows each
 // summing every 16th chunk, fixed-order combine in LDS (deterministic)
 __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ partial, int nchunk, int cols,
                                                             float* __restrict__ out, int accum, int round_bf16) {
@@ -87,7 +94,8 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restr
   __syncthreads();
   if (j == 0 && c < cols) {
     for (int k = 1; k < 16; ++k) t += st[k][cl];
-    if (round_bf16) t = rbf(t);
+    if (round_bf16 == 2) t = rnd<true>(t);
+    else if (round_bf16) t = rbf(t);
     out[c] = accum ? out[c] + t : t;
   }
 }
@@ -115,19 +123,22 @@ __global__ void finalize_norm_kernel(const float* __restrict__ partial, int nb, 
 
 // torch.optim.AdamW (foreach=False, non-capturable) with the clip_grad_norm_ factor fused:
 //   g *= min(1, max_norm / (norm + 1e-6)); p *= 1 - lr*wd; m = lerp(m, g, 1-b1);
-//   v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps);  optional bf16 copy of p.
+//   v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps);  optional 16-bit copy of p (H: fp16).
+// inv_scale (fp16 autocast's GradScaler.unscale_, a power of two): g and norm are the loss-scaled gradient and its
+// norm; g * inv_scale is the unscaled gradient exactly, and so is norm * inv_scale its norm (1.0 otherwise).
+template <bool H>
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, bf16* __restrict__ p_bf16, int64_t n, float lr, float b1, float b2,
                              float eps, float wd, float bc1, float bc2_sqrt, const float* __restrict__ norm,
-                             float max_norm) {
+                             float max_norm, float inv_scale) {
   float coef = 1.f;
   if (norm != nullptr && max_norm > 0.f) {
-    coef = max_norm / (norm[0] + 1e-6f);
+    coef = max_norm / (norm[0] * inv_scale + 1e-6f);
     coef = coef < 1.f ? coef : 1.f;
   }
   const float step_size = lr / bc1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = g[i] * coef;
+    const float gi = (g[i] * inv_scale) * coef;
     float pi = p[i];
     pi = pi * (1.f - lr * wd);
     float mi = m[i];
@@ -136,7 +147,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
     pi = pi - step_size * (mi / denom);
     p[i] = pi; m[i] = mi; v[i] = vi;
-    if (p_bf16) p_bf16[i] = f2bf(pi);
+    if (p_bf16) p_bf16[i] = f2e<H>(pi);
   }
 }
 
@@ -213,12 +224,13 @@ __global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, E* __res
   from_f32(xt[i], v);
 }
 
-// out = bf16( round?(g) * gelu'(pre) )  — GELU backward on an autocast bf16 activation
+// out = e( e(g) * gelu'(pre) )  — GELU backward on an autocast 16-bit activation (e = bf16, or fp16 for H)
+template <bool H>
 __global__ void gelu_bwd_kernel(const void* __restrict__ g, int g_dtype, const bf16* __restrict__ pre,
                                 bf16* __restrict__ out, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float gv = rbf(ld_as_f32(g, g_dtype, i));
-    out[i] = f2bf(gv * gelu_erf_grad(bf2f(pre[i])));
+    const float gv = rnd<H>(ld_as_f32(g, g_dtype, i));
+    out[i] = f2e<H>(gv * gelu_grad_of<H>(e2f<H>(pre[i])));
   }
 }
 
@@ -285,7 +297,16 @@ extern "C" int tw_transpose_bf16(const void* src, int64_t ld_src, int rows, int 
 
 extern "C" int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
   if (n <= 0) return TW_OK;
-  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(nblocks(n / 4 + 1, 256)), dim3(256), 0, stream, src, (bf16*)dst, n);
+  hipLaunchKernelGGL(cast_f32_bf16_kernel<false>, dim3(nblocks(n / 4 + 1, 256)), dim3(256), 0, stream, src, (bf16*)dst,
+                     n);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_cast_f32_f16(const float* src, void* dst, int64_t n, hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel<true>, dim3(nblocks(n / 4 + 1, 256)), dim3(256), 0, stream, src, (bf16*)dst,
+                     n);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }
@@ -313,17 +334,28 @@ extern "C" int tw_l2norm(const float* x, int64_t n, float* norm_out, float* work
   return TW_OK;
 }
 
+extern "C" int tw_adamw_ex(float* p, const float* g, float* m, float* v, void* p16, int p16_dtype, int64_t n, float lr,
+                           float b1, float b2, float eps, float wd, int step, const float* norm, float max_norm,
+                           float inv_scale, hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  if (step < 1 || !(inv_scale > 0.f)) return TW_EINVAL;
+  if (p16 && p16_dtype != TW_BF16 && p16_dtype != TW_F16) return TW_EINVAL;
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  if (p16 && p16_dtype == TW_F16)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, p, g, m, v, (bf16*)p16, n,
+                       lr, b1, b2, eps, wd, bc1, sqrtf(bc2), norm, max_norm, inv_scale);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, p, g, m, v, (bf16*)p16,
+                       n, lr, b1, b2, eps, wd, bc1, sqrtf(bc2), norm, max_norm, inv_scale);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
 extern "C" int tw_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float b1,
                         float b2, float eps, float wd, int step, const float* norm, float max_norm,
                         hipStream_t stream) {
-  if (n <= 0) return TW_OK;
-  if (step < 1) return TW_EINVAL;
-  const float bc1 = 1.f - powf(b1, (float)step);
-  const float bc2 = 1.f - powf(b2, (float)step);
-  hipLaunchKernelGGL(adamw_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, p, g, m, v, (bf16*)p_bf16, n, lr,
-                     b1, b2, eps, wd, bc1, sqrtf(bc2), norm, max_norm);
-  TW_CHECK_LAUNCH();
-  return TW_OK;
+  return tw_adamw_ex(p, g, m, v, p_bf16, TW_BF16, n, lr, b1, b2, eps, wd, step, norm, max_norm, 1.0f, stream);
 }
 
 extern "C" int tw_clip_scale(float* x, int64_t n, const float* norm, float max_norm, hipStream_t stream) {
@@ -386,8 +418,16 @@ extern "C" int tw_mel_to_conv_input_f16(const float* mel, void* xt, int B, int n
 
 extern "C" int tw_gelu_bwd(const void* g, int g_dtype, const void* pre, void* out, int64_t n, hipStream_t stream) {
   if (n <= 0) return TW_OK;
-  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, g, g_dtype, (const bf16*)pre,
-                     (bf16*)out, n);
+  hipLaunchKernelGGL(gelu_bwd_kernel<false>, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, g, g_dtype,
+                     (const bf16*)pre, (bf16*)out, n);
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+extern "C" int tw_gelu_bwd_f16(const void* g, int g_dtype, const void* pre, void* out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return TW_OK;
+  hipLaunchKernelGGL(gelu_bwd_kernel<true>, dim3(nblocks(n, 256, 8192)), dim3(256), 0, stream, g, g_dtype,
+                     (const bf16*)pre, (bf16*)out, n);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -63,6 +63,12 @@ SIGNATURES = {
                     P, I64, I64, I32, P, P],
     "tw_attn_fwd_f16": [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, F32, P],
     "tw_mel_to_conv_input_f16": [P, P, I32, I32, I32, P],
+    # fp16-autocast training (run_distillation.py:815-817 --dtype float16)
+    "tw_attn_bwd_f16": [P, I64, P, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, I32, I32, I32, I32,
+                        I32, I32, F32, P, P],
+    "tw_gelu_bwd_f16": [P, I32, P, P, I64, P],
+    "tw_cast_f32_f16": [P, P, I64, P],
+    "tw_adamw_ex": [P, P, P, P, P, I32, I64, F32, F32, F32, F32, F32, I32, P, F32, F32, P],
     # fp32 arithmetic path
     "tw_gemm_f32": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I64, I64, I64, I32, I64, I64, I64, F32,
                     P, P, I64, I64, I32, P, I64, I64, I32, P],

@@ -71,6 +71,42 @@ def weight_decay_runs(s: WhisperForConditionalGeneration, wd: float, freeze_enco
     return [tuple(r) for r in runs]
 
 
+class GradScaler:
+    """torch.amp.GradScaler as accelerate builds it for mixed_precision="fp16" (run_distillation.py:815-827; ACC
+    accelerator.py: GradScaler(**kwargs) with the defaults): the loss gradient is multiplied by `scale`; at the sync
+    micro-step a non-finite gradient norm skips the optimizer step (and, in accelerate, the scheduler step) and halves
+    the scale, else the step runs on gradient / scale and after `growth_interval` finite steps in a row the scale
+    doubles.  Host-side state: the engine reads the norm once per update to decide (torch's GradScaler.step reads
+    found_inf the same way)."""
+
+    def __init__(self, init_scale=65536.0, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000):
+        self.scale = float(init_scale)
+        self.growth_factor, self.backoff_factor = float(growth_factor), float(backoff_factor)
+        self.growth_interval = int(growth_interval)
+        self.growth_tracker = 0
+
+    def update(self, found_inf: bool):
+        """GradScaler.update (torch _amp_update_scale_)."""
+        if found_inf:
+            self.scale *= self.backoff_factor
+            self.growth_tracker = 0
+        else:
+            self.growth_tracker += 1
+            if self.growth_tracker == self.growth_interval:
+                self.scale *= self.growth_factor
+                self.growth_tracker = 0
+
+    def state_dict(self):
+        return {"scale": self.scale, "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
+                "growth_interval": self.growth_interval, "_growth_tracker": self.growth_tracker}
+
+    def load_state_dict(self, sd):
+        self.scale = float(sd["scale"])
+        self.growth_factor, self.backoff_factor = float(sd["growth_factor"]), float(sd["backoff_factor"])
+        self.growth_interval = int(sd["growth_interval"])
+        self.growth_tracker = int(sd["_growth_tracker"])
+
+
 class DistillationTrainer:
     def __init__(self, student: WhisperForConditionalGeneration, teacher: WhisperForConditionalGeneration, *,
                  temperature: float = 2.0, kl_weight: float = 1.0, learning_rate: float = 1e-4,
@@ -111,6 +147,16 @@ class DistillationTrainer:
         self.overlap_update = (self.dp and freeze_encoder) if overlap_update is None else bool(overlap_update)
         if self.overlap_update and not freeze_encoder:
             raise ValueError("overlap_update needs a frozen encoder: the next forward must read no trainable weight")
+        # fp16 autocast (--dtype float16): dynamic loss scaling.  Whether an update runs depends on the norm of the
+        # exchanged gradient, read on the host at the sync micro-step, so the update is never deferred.
+        self.scaler = GradScaler() if student.compute == "fp16" else None
+        if self.scaler is not None:
+            if student.dtype != torch.float32:
+                raise ValueError("fp16 distillation trains an fp32-master student under fp16 autocast")
+            if overlap_update:
+                raise ValueError("overlap_update: the fp16 loss scaler decides each update on the host")
+            self.overlap_update = False
+        self.skipped_steps = 0   # fp16: optimizer steps skipped for a non-finite gradient (GradScaler)
         self._update = None      # (lr, t) of a launched, not yet applied update
         # bench.py instrumentation: with lists here, wait_grad_exchange() appends (start, layers done, tail done)
         # events around each exchange wait and _launch() appends (bytes, tail) per all-reduced slice
@@ -198,8 +244,12 @@ class DistillationTrainer:
         lab = labels.reshape(-1)
         F.count_valid(lab, self.nvalid)
         dlogits = torch.empty_like(ls)
+        # the loss gradient: 1 / accum (accelerate's backward), the folded DDP mean, and fp16's loss scale
+        # (scaler.scale(loss).backward(): the scale enters the fp32 gradient before its fp16 rounding)
+        gs = (self.scaler.scale if self.scaler is not None else 1.0) / (self.accum * (self.world if self.fold_world
+                                                                                         else 1))
         out3, _ = F.kl_ce(ls, lt, lab, s.config.vocab_size, self.nvalid, T=T, ce_w=0.8, kl_w=self.kl_weight,
-                          grad_scale=1.0 / (self.accum * (self.world if self.fold_world else 1)), dlogits=dlogits)
+                          grad_scale=gs, dlogits=dlogits)
         del lt
         d_enc = torch.zeros(B * Tk, s.config.d_model, dtype=torch.float32, device=s.device) \
             if self.train_encoder else None
@@ -297,25 +347,39 @@ class DistillationTrainer:
         self.wait_grad_exchange()
 
     def _apply_update(self, lr, t):
+        """Clip + AdamW; returns False when the fp16 loss scaler skipped the step (non-finite gradient norm)."""
         s = self.s
         self.wait_grad_exchange()
         g = s.grad
         F.l2norm(g, self.norm, self.ws)
+        inv = 1.0
+        if self.scaler is not None:
+            # GradScaler.unscale_ + clip_grad_norm_ + step: the norm of the scaled gradient is finite iff every
+            # element is (up to an fp32 overflow of the sum of squares); unscaling by a power of two is exact, so
+            # adamw_ex applies g / scale and norm / scale inside the update kernel
+            found_inf = not math.isfinite(float(self.norm.item()))
+            scale = self.scaler.scale
+            self.scaler.update(found_inf)
+            if found_inf:
+                self.skipped_steps += 1
+                return False
+            inv = 1.0 / scale
         for lo, hi, wd in self.runs:
             F.adamw(s.store.p32[lo:hi], g[lo:hi], self.m_buf[lo:hi], self.v_buf[lo:hi], s.store.p16[lo:hi], lr,
-                    self.b1, self.b2, self.eps, wd, t, self.norm, self.max_grad_norm)
+                    self.b1, self.b2, self.eps, wd, t, self.norm, self.max_grad_norm, inv_scale=inv)
+        return True
 
     def optimizer_step(self):
         """Clip + AdamW on the exchanged gradient.  With overlap_update the exchange is launched here and the
         update is applied by the next flush() (the next train_step, after its encoder forward); `self.norm`
         holds the clipped-over norm once it has run."""
         lr, t = self.lr_at(self.step), self.step + 1
-        self.step += 1
         self.launch_grad_exchange()
         if self.overlap_update:
+            self.step += 1
             self._update = (lr, t)
-        else:
-            self._apply_update(lr, t)
+        elif self._apply_update(lr, t):
+            self.step += 1     # a skipped fp16 step leaves AdamW's step count and the schedule where they were
         return self.norm
 
     def flush(self):
@@ -410,6 +474,8 @@ class DistillationTrainer:
                           metadata={"format": "pt"})
             torch.save(self.optimizer_state_dict(), os.path.join(output_dir, "optimizer.bin"))
             torch.save(self.scheduler_state_dict(), os.path.join(output_dir, "scheduler.bin"))
+            if self.scaler is not None:     # accelerator.save_state writes the fp16 GradScaler as scaler.pt
+                torch.save(self.scaler.state_dict(), os.path.join(output_dir, "scaler.pt"))
         torch.save({"torch_manual_seed": torch.get_rng_state(), "step": self.step},
                    os.path.join(output_dir, f"random_states_{rank}.pkl"))
 
@@ -424,6 +490,9 @@ class DistillationTrainer:
         self.s.sync_bf16()
         opt = torch.load(os.path.join(input_dir, "optimizer.bin"), map_location="cpu", weights_only=True)
         self.load_optimizer_state_dict(opt)
+        cp = os.path.join(input_dir, "scaler.pt")
+        if self.scaler is not None and os.path.exists(cp):
+            self.scaler.load_state_dict(torch.load(cp, map_location="cpu", weights_only=True))
         sp = os.path.join(input_dir, "scheduler.bin")
         if os.path.exists(sp):
             sch = torch.load(sp, map_location="cpu", weights_only=True)

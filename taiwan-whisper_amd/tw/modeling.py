@@ -210,8 +210,9 @@ class WhisperForConditionalGeneration:
         arithmetic end to end (mixed_precision="no", the reference's default --dtype float32; needs the
         fp32 master); "fp16" = a torch_dtype=float16 model without autocast (run_eval.py:99,500-509 default
         --dtype float16, run_pseudo_labelling.py:461-463): fp16 weights, fp16 Linear / attention outputs and
-        residual stream, LayerNorm statistics in fp32 with fp16 output, fp16 logits.  An fp16 model is
-        inference-only (the reference trains in bf16 or fp32)."""
+        residual stream, LayerNorm statistics in fp32 with fp16 output, fp16 logits -- inference and the fp16
+        teacher of fp16 distillation; on an fp32-master model "fp16" is CUDA fp16 AUTOCAST (mixed_precision="fp16",
+        run_distillation.py:815-817): the bf16 path's rounding points with fp16 in place of bf16 (fp32 stream)."""
         if isinstance(config, dict):
             config = WhisperConfig(**config)
         self.config = config
@@ -223,7 +224,7 @@ class WhisperForConditionalGeneration:
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             raise ValueError(f"unsupported parameter dtype {dtype}")
         self.store = ParamStore(self.segs, self.device, master=(dtype == torch.float32),
-                                half=torch.float16 if dtype == torch.float16 else torch.bfloat16)
+                                half=torch.float16 if (dtype == torch.float16 or compute == "fp16") else torch.bfloat16)
         self._ln32 = {}          # fp32 LayerNorm params for bf16 models
         self.trainable = set()   # HF names with requires_grad
         self.grad = None         # flat fp32 grads over the trainable prefix (see pack_for_training)
@@ -241,9 +242,16 @@ class WhisperForConditionalGeneration:
             raise ValueError(f"compute must be 'bf16', 'fp16' or 'fp32', got {compute!r}")
         if compute == "fp32" and self.dtype != torch.float32:
             raise ValueError("fp32 arithmetic needs fp32 parameters (torch_dtype=torch.float32)")
-        if (compute == "fp16") != (self.dtype == torch.float16):
-            raise ValueError("fp16 arithmetic is the torch_dtype=float16 model (fp16 parameters), and only that")
+        if self.dtype == torch.float16 and compute != "fp16":
+            raise ValueError("a torch_dtype=float16 model computes in fp16 only")
+        if self.dtype == torch.bfloat16 and compute == "fp16":
+            raise ValueError("fp16 arithmetic needs fp16 parameters or an fp32 master (fp16 autocast)")
         self.compute = compute
+        # fp32-master model: the 16-bit mirror is autocast's weight cast, in the autocast dtype
+        half = torch.float16 if compute == "fp16" else torch.bfloat16
+        if self.store.p32 is not None and compute != "fp32" and self.store.p16.dtype != half:
+            self.store.p16 = torch.empty(self.store.total, dtype=half, device=self.device)
+            F.cast_bf16(self.store.p32, self.store.p16)
         return self
 
     @property
@@ -253,9 +261,9 @@ class WhisperForConditionalGeneration:
         return {"fp32": torch.float32, "fp16": torch.float16}.get(self.compute, torch.bfloat16)
 
     def act_grad(self, g: torch.Tensor) -> torch.Tensor:
-        """gradient entering a GEMM: rounded to bf16 under autocast (the grad of a bf16 activation),
+        """gradient entering a GEMM: rounded to the autocast dtype (the grad of a bf16 / fp16 activation),
         unchanged on the fp32 path."""
-        return g if self.compute == "fp32" else _bf16(g)
+        return g if self.compute == "fp32" else _half(g, self.act_dtype)
 
     # ------------------------------------------------------------------ state dict / IO
     @property
@@ -380,7 +388,7 @@ class WhisperForConditionalGeneration:
         tr = [n for n in names if (owner(n) in self.trainable)]
         fr = [n for n in names if owner(n) not in self.trainable]
         old = self.store
-        new = ParamStore(self.segs, self.device, master=True, order=tr + fr)
+        new = ParamStore(self.segs, self.device, master=True, order=tr + fr, half=old.p16.dtype)
         for n in names:
             new.v32(n).copy_(old.v32(n))
             new.v16(n).copy_(old.v16(n))
@@ -415,7 +423,7 @@ class WhisperForConditionalGeneration:
         return None if lo is None else (lo, hi)
 
     def sync_bf16(self):
-        """bf16 mirror := bf16(fp32 master) (autocast's weight cast) for the whole model."""
+        """16-bit mirror := bf16 / fp16 (fp32 master) (autocast's weight cast) for the whole model."""
         if self.store.p32 is not None:
             F.cast_bf16(self.store.p32, self.store.p16)
 
@@ -484,7 +492,8 @@ class WhisperForConditionalGeneration:
             self._lin(h, w, b, r)
             return x, r
         out = torch.empty(M, N, dtype=self.stream_dtype, device=self.device) if tape is not None else x
-        flags = F.GEMM_ROUND | (F.GEMM_CLAMP16 if clamp and self.compute == "fp16" else 0)
+        # HF clamps only an fp16 STREAM (modeling_whisper.py:409-411): the fp16 model's, not fp16 autocast's fp32 one
+        flags = F.GEMM_ROUND | (F.GEMM_CLAMP16 if clamp and self.stream_dtype == torch.float16 else 0)
         self._lin(h, w, b, out, res=x, flags=flags)
         return out, None
 
@@ -687,8 +696,8 @@ class WhisperForConditionalGeneration:
 # points: weight/bias grads of bf16 Linears are rounded to bf16 before the fp32 accumulate
 # (the grad of the autocast weight cast), activation grads entering a bf16 tensor are rounded.
 # =============================================================================================
-def _bf16(x: torch.Tensor) -> torch.Tensor:
-    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+def _half(x: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
     F.cast_bf16(x.contiguous(), out)
     return out
 
@@ -726,9 +735,9 @@ class Backward:
     def dX(self, g, w, out, flags=F.GEMM_ROUND, aux=None, M=None):
         M = g.shape[0] if M is None else M
         N, K = w.shape
-        if (M >= 4096 and flags == F.GEMM_ROUND and aux is None and w.dtype == torch.bfloat16 and g.dtype == w.dtype
-                and out.dtype == torch.bfloat16):
-            wt = F.transpose_bf16(w, torch.empty(K, N, dtype=torch.bfloat16, device=self.dev))
+        if (M >= 4096 and flags == F.GEMM_ROUND and aux is None and w.dtype in F.HALF and g.dtype == w.dtype
+                and out.dtype == w.dtype):
+            wt = F.transpose_bf16(w, torch.empty(K, N, dtype=w.dtype, device=self.dev))
             F.gemm(g, wt, out, M, K, N, lda=g.stride(0), ldb=N, ldc=out.stride(0), flags=flags)
         else:
             F.gemm(g, w, out, M, K, N, lda=g.stride(0), ldb=K, ldc=out.stride(0), b_trans=True, aux=aux,
@@ -740,7 +749,7 @@ class Backward:
             return
         lo, hi = cols_slice
         F.colsum(g[:, lo:] if lo else g, g.stride(0), g.shape[0], hi - lo, out, accum=True,
-                 round_bf16=self.m.compute != "fp32")
+                 round_bf16={"fp32": 0, "fp16": 2}.get(self.m.compute, 1))
 
     def ln(self, sv, name, dy, dx):
         x, mean, rstd, _ = sv[name]
@@ -832,11 +841,11 @@ class Backward:
         M = h16.shape[0]
         E16 = m._w16("model.decoder.embed_tokens.weight")
         gE = m.gv("model.decoder.embed_tokens.weight")
-        # LM head (tied): dh = bf16(dlogits E), dE += bf16(dlogits^T h).  On the bf16 path E goes K-major first
-        # (one 133 MB transpose): the K = 51 904 product then runs on the persistent kernel
+        # LM head (tied): dh = e(dlogits E), dE += e(dlogits^T h) (e = the autocast dtype).  On the 16-bit paths E goes
+        # K-major first (one 133 MB transpose): the K = 51 904 product then runs on the persistent kernel
         dh = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
-        if E16.dtype == torch.bfloat16 and M >= 4096:
-            ET = F.transpose_bf16(E16, torch.empty(d, m.Vp, dtype=torch.bfloat16, device=self.dev))
+        if E16.dtype in F.HALF and M >= 4096:
+            ET = F.transpose_bf16(E16, torch.empty(d, m.Vp, dtype=E16.dtype, device=self.dev))
             F.gemm(dlogits, ET, dh, M, d, m.Vp, lda=m.Vp, ldb=m.Vp, ldc=d, flags=F.GEMM_ROUND)
             del ET
         else:

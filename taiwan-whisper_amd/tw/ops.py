@@ -53,8 +53,8 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
          ldr=0, res_mod=0, aux=None, ldaux=0, flags=0, batch=1, sA=0, sB=0, sC=0, sR=0, sAux=0, algo_N=None,
          batch_inner=1, sA_in=0, sB_in=0, sC_in=0):
     """C[b] = epi(alpha * A[b] @ B[b]^T); A [M][K] (a_trans: [K][M]); B [N][K] (b_trans: [K][N]).
-    bf16 operands -> tw_gemm_bf16 (autocast rounding points); fp16 operands -> tw_gemm_f16 (the fp16 model:
-    K-major operands only, every 16-bit tensor fp16); fp32 operands -> tw_gemm_f32 (the fp32 path: every
+    bf16 operands -> tw_gemm_bf16 (autocast rounding points); fp16 operands -> tw_gemm_f16 (the fp16 model and
+    fp16-autocast training: every 16-bit tensor fp16); fp32 operands -> tw_gemm_f32 (the fp32 path: every
     operand and epilogue tensor fp32, nothing rounded)."""
     if M <= 0 or N <= 0:
         return C
@@ -66,8 +66,6 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     assert batch_inner == 1, "tw.gemm: two-level batches are an fp32-path feature"
     h = A.dtype
     assert h in HALF and B.dtype == h, "tw.gemm: A and B must be both bf16, both fp16 (or both fp32)"
-    if h == torch.float16:
-        assert not a_trans and not b_trans, "tw.gemm: fp16 products are forward-only (K-major A and B)"
     assert C.dtype in (h, torch.float32), "tw.gemm: C is the operand dtype or fp32"
     _need(A, (batch - 1) * sA + ((K - 1) * lda + M if a_trans else (M - 1) * lda + K), "gemm A")
     _need(B, (batch - 1) * sB + ((K - 1) * ldb + N if b_trans else (N - 1) * ldb + K), "gemm B")
@@ -193,12 +191,12 @@ def attn_bwd(q, ldq, k, ldk, v, ldv, o, ldo, do, lddo, lse, dq, lddq, dk, lddk, 
     hd = 64
     for t, ld, T, nm in ((q, ldq, Tq, "q"), (k, ldk, Tk, "k"), (v, ldv, Tk, "v"), (o, ldo, Tq, "o"),
                          (do, lddo, Tq, "do"), (dq, lddq, Tq, "dq"), (dk, lddk, Tk, "dk"), (dv, lddv, Tk, "dv")):
-        assert t.dtype == torch.bfloat16, nm
+        assert t.dtype == q.dtype and t.dtype in HALF, nm
         _need(t, (B * T - 1) * ld + H * hd, f"attn_bwd {nm}")
     _need(lse, B * H * Tq, "attn lse")
     if workspace is None or workspace.numel() < B * H * Tq:
         workspace = torch.empty(B * H * Tq, dtype=torch.float32, device=q.device)
-    call("tw_attn_bwd", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, do.data_ptr(),
+    call("tw_attn_bwd_f16" if q.dtype == torch.float16 else "tw_attn_bwd", q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv, o.data_ptr(), ldo, do.data_ptr(),
          lddo, lse.data_ptr(), dq.data_ptr(), lddq, dk.data_ptr(), lddk, dv.data_ptr(), lddv, B, H, Tq, Tk, hd,
          int(causal), float(scale), workspace.data_ptr(), _stream())
 
@@ -273,9 +271,9 @@ def embed_bwd(ids, dh, dE, padding_idx=-1):
 
 
 def transpose_bf16(src, dst):
-    """dst [cols][rows] = src [rows][cols]^T (bf16, both row-major, dst contiguous)."""
+    """dst [cols][rows] = src [rows][cols]^T (16-bit words: bf16 or fp16, both row-major, dst contiguous)."""
     rows, cols = src.shape
-    assert src.dtype == torch.bfloat16 and dst.dtype == torch.bfloat16 and src.stride(1) == 1
+    assert src.dtype in HALF and dst.dtype == src.dtype and src.stride(1) == 1
     assert dst.is_contiguous() and tuple(dst.shape) == (cols, rows) and src.is_cuda and dst.is_cuda
     _need(src, (rows - 1) * src.stride(0) + cols, "transpose src")
     call("tw_transpose_bf16", src.data_ptr(), src.stride(0), rows, cols, dst.data_ptr(), rows, _stream())
@@ -283,9 +281,12 @@ def transpose_bf16(src, dst):
 
 
 def cast_bf16(src, dst):
-    assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() <= dst.numel()
+    """fp32 -> the 16-bit dtype of dst (bf16: tw_cast_f32_bf16, fp16: tw_cast_f32_f16), RNE: autocast's weight cast
+    and the rounding of a gradient entering a 16-bit GEMM operand."""
+    assert src.dtype == torch.float32 and dst.dtype in HALF and src.numel() <= dst.numel()
     assert src.is_contiguous() and dst.is_contiguous()
-    call("tw_cast_f32_bf16", src.data_ptr(), dst.data_ptr(), src.numel(), _stream())
+    call("tw_cast_f32_f16" if dst.dtype == torch.float16 else "tw_cast_f32_bf16", src.data_ptr(), dst.data_ptr(),
+         src.numel(), _stream())
     return dst
 
 
@@ -303,6 +304,7 @@ def workspace(n, device, key="ws"):
 
 
 def colsum(x, ldx, rows, cols, out, accum=True, round_bf16=True):
+    """out (+)= [round](column sums of x); round_bf16: False / True (bf16) / 2 (fp16)."""
     _need(x, (rows - 1) * ldx + cols, "colsum x")
     assert out.dtype == torch.float32 and out.numel() >= cols
     n = (rows + 255) // 256 * cols
@@ -317,13 +319,20 @@ def l2norm(x, out, workspace):
     return out
 
 
-def adamw(p, g, m, v, p_bf16, lr, b1, b2, eps, wd, step, norm=None, max_norm=0.0):
+def adamw(p, g, m, v, p_bf16, lr, b1, b2, eps, wd, step, norm=None, max_norm=0.0, inv_scale=1.0):
+    """Clip + AdamW (+ the 16-bit weight copy, bf16 or fp16 by p_bf16's dtype).  inv_scale != 1: g / norm are the
+    loss-scaled gradient and its norm (fp16 autocast's GradScaler; 1 / scale, a power of two)."""
     n = p.numel()
     assert g.numel() == n and m.numel() == n and v.numel() == n
     if p_bf16 is not None:
-        assert p_bf16.numel() >= n and p_bf16.dtype == torch.bfloat16
-    call("tw_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(p_bf16), n, float(lr), float(b1),
-         float(b2), float(eps), float(wd), int(step), _ptr(norm), float(max_norm), _stream())
+        assert p_bf16.numel() >= n and p_bf16.dtype in HALF
+    if inv_scale == 1.0 and (p_bf16 is None or p_bf16.dtype == torch.bfloat16):
+        call("tw_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(p_bf16), n, float(lr), float(b1),
+             float(b2), float(eps), float(wd), int(step), _ptr(norm), float(max_norm), _stream())
+        return
+    call("tw_adamw_ex", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _ptr(p_bf16),
+         F16 if p_bf16 is not None and p_bf16.dtype == torch.float16 else BF16, n, float(lr), float(b1), float(b2),
+         float(eps), float(wd), int(step), _ptr(norm), float(max_norm), float(inv_scale), _stream())
 
 
 def im2col3(src, src_rows, dst, B, T_out, stride, C):
@@ -359,8 +368,9 @@ def gelu_bwd(g, pre, out):
         assert g.dtype == torch.float32 and out.dtype == torch.float32
         call("tw_gelu_bwd_f32", g.data_ptr(), pre.data_ptr(), out.data_ptr(), g.numel(), _stream())
         return out
-    assert pre.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
-    call("tw_gelu_bwd", g.data_ptr(), _dt(g), pre.data_ptr(), out.data_ptr(), g.numel(), _stream())
+    assert pre.dtype in HALF and out.dtype == pre.dtype
+    call("tw_gelu_bwd_f16" if pre.dtype == torch.float16 else "tw_gelu_bwd", g.data_ptr(), _dt(g), pre.data_ptr(),
+         out.data_ptr(), g.numel(), _stream())
     return out
 
 

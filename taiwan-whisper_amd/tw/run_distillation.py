@@ -182,20 +182,18 @@ def evaluate(trainer, feed, tokenizer, gen_kwargs: dict, predict_with_generate: 
 
 def teacher_dtype(dtype: str):
     """--dtype -> teacher weight dtype (run_distillation.py:815-823).  bfloat16 = bf16 autocast
-    (mixed_precision="bf16"); float32 = mixed_precision="no" (fp32 arithmetic end to end, the
-    reference's default).  float16 (fp16 autocast + grad scaler) is not implemented and raises
-    rather than silently running another precision."""
+    (mixed_precision="bf16"); float16 = fp16 autocast with the dynamic loss scaler (mixed_precision="fp16",
+    fp16 teacher); float32 = mixed_precision="no" (fp32 arithmetic end to end, the reference's default)."""
     if dtype == "bfloat16":
         return torch.bfloat16
+    if dtype == "float16":
+        return torch.float16
     if dtype == "float32":
         from .modeling import fp32_compute_supported
         if not fp32_compute_supported():
             raise NotImplementedError("--dtype float32 (mixed_precision='no') needs the fp32 arithmetic path")
         return torch.float32
-    raise NotImplementedError(f"--dtype {dtype}: distillation trains in bfloat16 or float32 (every reference "
-                              "launcher uses bfloat16); fp16 autocast with a dynamic loss scaler is not implemented. "
-                              "fp16 INFERENCE (torch_dtype=float16: run_eval.py / pseudo-labelling) is: "
-                              "WhisperForConditionalGeneration.from_pretrained(dir, torch_dtype=torch.float16)")
+    raise ValueError(f"--dtype {dtype}: one of float32, float16, bfloat16 (run_distillation.py:417-424)")
 
 
 def load_models(args, device, tokenizer=None):
@@ -204,7 +202,8 @@ def load_models(args, device, tokenizer=None):
     creation (create_student_model.py:124-125)."""
     from .modeling import WhisperForConditionalGeneration
     from .student import mix_language_embeddings
-    compute = "fp32" if args.dtype == "float32" else "bf16"      # mixed_precision "no" / "bf16" (:815-823)
+    # mixed_precision "no" / "fp16" / "bf16" (:815-823)
+    compute = {"float32": "fp32", "float16": "fp16"}.get(args.dtype, "bf16")
     teacher = WhisperForConditionalGeneration.from_pretrained(args.teacher_model_name_or_path,
                                                               torch_dtype=teacher_dtype(args.dtype), device=device,
                                                               compute=compute)

@@ -707,12 +707,13 @@ def _trainable(names, freeze_encoder, freeze_embed_positions):
     return out
 
 
-def run_hf_step(S, T, feats, dec, lab, share, amp, temperature=2.0):
+def run_hf_step(S, T, feats, dec, lab, share, amp, temperature=2.0, amp_dtype=torch.bfloat16, scaler=None):
     """The reference train_step (run_distillation.py:1519-1551) on HF modules; returns scalars, the
-    fp32 (upcast) logits and the encoder output; gradients land on S's parameters."""
+    fp32 (upcast) logits and the encoder output; gradients land on S's parameters (loss-scaled when a
+    GradScaler is given: accelerator.backward under mixed_precision="fp16" is scaler.scale(loss).backward())."""
     import contextlib
     from transformers.modeling_outputs import BaseModelOutput
-    ctx = (lambda: torch.autocast("cpu", dtype=torch.bfloat16)) if amp else contextlib.nullcontext
+    ctx = (lambda: torch.autocast("cpu", dtype=amp_dtype)) if amp else contextlib.nullcontext
     with ctx():
         so = S(input_features=feats, decoder_input_ids=dec, labels=lab)
     s_logits = so.logits.float()
@@ -729,7 +730,7 @@ def run_hf_step(S, T, feats, dec, lab, share, amp, temperature=2.0):
     mask = (lab >= 0).unsqueeze(-1)
     kl = (torch.nn.functional.kl_div(lq, p, reduction="none") * mask).sum() / mask.sum() * temperature ** 2
     loss = 0.8 * ce + kl
-    loss.backward()
+    (scaler.scale(loss) if scaler is not None else loss).backward()
     return dict(loss=loss.detach(), ce=ce.detach(), kl=kl.detach(), s_logits=s_logits.detach(),
                 t_logits=t_logits.detach(), enc=enc.detach().float())
 
@@ -774,9 +775,60 @@ def gen_cfg(case, out):
         del S, T, r
 
 
+def gen_cfg_f16(case, out):
+    """The fp16-autocast rows of a BASELINE-config fixture (mixed_precision="fp16", run_distillation.py:815-817):
+    the student under torch.autocast(float16), the teacher's weights in fp16 (teacher_dtype), the loss through a
+    default GradScaler (init scale 2^16; accelerate's fp16 path) -- unscale_ before the gradient norms and
+    clip_grad_norm_, then scaler.step (AdamW) and scaler.update.  Keys "f16|..." merged into the existing file."""
+    import time
+    c = CFG_CASES[case]
+    t0 = time.time()
+    scfg, ws, tcfg, wt = cfg_case_weights(case)
+    feats, dec, lab = cfg_case_batch(case)
+    ft, dt, lt = torch.from_numpy(feats), torch.from_numpy(dec), torch.from_numpy(lab)
+    share = c["freeze_encoder"] and scfg["d_model"] == tcfg["d_model"]
+    S = hf_model(scfg, ws).train()
+    T = hf_model(tcfg, wt, torch.float16).eval()
+    tr = [n for n in out["grad_names"]]
+    for n, p_ in S.named_parameters():
+        p_.requires_grad_(n in tr)
+    scaler = torch.amp.GradScaler("cpu")
+    r = run_hf_step(S, T, ft, dt, lt, share, amp=True, amp_dtype=torch.float16, scaler=scaler)
+    mode = "f16"
+    out[f"{mode}|loss"], out[f"{mode}|ce"], out[f"{mode}|kl"] = (np.float64(r[k].item()) for k in ("loss", "ce", "kl"))
+    out[f"{mode}|s_lse"] = torch.logsumexp(r["s_logits"], -1).numpy()
+    out[f"{mode}|t_lse"] = torch.logsumexp(r["t_logits"], -1).numpy()
+    out[f"{mode}|s_argmax"] = r["s_logits"].argmax(-1).numpy()
+    out[f"{mode}|s_rows"] = r["s_logits"][:, ROWS, ::VSTRIDE].numpy()
+    out[f"{mode}|enc_sub"] = r["enc"][:, ::50, :].numpy()
+    tp = [S.get_parameter(n) for n in tr]
+    opt = torch.optim.AdamW(tp, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
+    out[f"{mode}|scale"] = np.float64(scaler.get_scale())
+    scaler.unscale_(opt)
+    out[f"{mode}|grad_norms"] = np.array([S.get_parameter(n).grad.double().norm().item() for n in tr])
+    p0 = "model.decoder.layers.0.fc1.weight"
+    out[f"{mode}|grad_dec0_fc1_sub"] = S.get_parameter(p0).grad[::37, ::29].clone().numpy()
+    gn = torch.nn.utils.clip_grad_norm_(tp, 1.0)
+    scaler.step(opt)
+    scaler.update()
+    out[f"{mode}|grad_total_norm"] = np.float64(gn.item())
+    out[f"{mode}|scale_after"] = np.float64(scaler.get_scale())
+    out[f"{mode}|upd_dec0_fc1_sub"] = S.get_parameter(p0).detach()[::37, ::29].clone().numpy()
+    print(case, mode, {k: float(r[k]) for k in ("loss", "ce", "kl")}, "scale", scaler.get_scale(),
+          round(time.time() - t0, 1), "s", flush=True)
+
+
 def main():
     torch.manual_seed(0)
     only = sys.argv[1:]
+    if only and only[0] == "f16":       # make_golden.py f16 c1 c2 ...: add the fp16-autocast rows to cfg fixtures
+        for case in only[1:]:
+            path = os.path.join(HERE, f"cfg_{case}.npz")
+            z = np.load(path)
+            out = {k: z[k] for k in z.files if not k.startswith("f16|")}
+            gen_cfg_f16(case, out)
+            np.savez_compressed(path, **out)
+        return
     for name, fn in (("mel", gen_mel), ("mel_long", gen_mel_long), ("micro_step", gen_micro), ("student", gen_student), ("greedy", gen_greedy), ("beam", gen_beam), ("beam_ts", gen_beam_ts),
                      ("greedy_ts", gen_greedy_ts), ("fallback", gen_fallback), ("fp16", gen_fp16),
                      ("lv2_decode", gen_lv2_decode), ("batched_longform", gen_batched_longform),

@@ -151,7 +151,7 @@ def test_partial_accumulation_steps_at_end_of_dataloader():
 def test_entry_point_float32_dtype(tmp_path):
     """--dtype float32 (the reference's default: mixed_precision="no", teacher in fp32,
     run_distillation.py:815-823) trains and evaluates on the fp32 arithmetic path; --dtype float16
-    raises instead of silently running another precision."""
+    (mixed_precision="fp16": fp16 teacher, fp16 autocast, dynamic loss scaling) trains and evaluates too."""
     from tw.run_distillation import main
     teacher, student = _model_dirs(str(tmp_path))
     man = _corpus(str(tmp_path / "corpus"))
@@ -165,5 +165,8 @@ def test_entry_point_float32_dtype(tmp_path):
     res = main(common + ["--dtype", "float32"])
     assert [h["step"] for h in res["train"]] == [1, 2]
     assert all(np.isfinite(h["loss"]) for h in res["train"]) and np.isfinite(res["eval"][0]["loss"])
-    with pytest.raises(NotImplementedError):
-        main(common + ["--dtype", "float16", "--output_dir", str(tmp_path / "out16")])
+    res16 = main(common + ["--dtype", "float16", "--output_dir", str(tmp_path / "out16")])
+    assert [h["step"] for h in res16["train"]] == [1, 2]
+    assert all(np.isfinite(h["loss"]) for h in res16["train"]) and np.isfinite(res16["eval"][0]["loss"])
+    # same data and weights: the fp16 run's first loss is the fp32 run's up to fp16 rounding
+    assert abs(res16["train"][0]["loss"] - res["train"][0]["loss"]) <= 2e-2 * abs(res["train"][0]["loss"])
