@@ -63,19 +63,27 @@ def make_models(args, device):
     small = dict(d_model=768, encoder_layers=12, decoder_layers=12, encoder_attention_heads=12,
                  decoder_attention_heads=12, encoder_ffn_dim=3072, decoder_ffn_dim=3072)
     tcfg = WhisperConfig(**large)
+    # --dtype bf16 (every reference launcher) or fp16 (--dtype float16: fp16 teacher, fp16-autocast student + loss
+    # scaler, run_distillation.py:815-817)
+    tdt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     if args.config == "c3":
         t32 = random_init_(WhisperForConditionalGeneration(tcfg, dtype=torch.float32, device=device), seed=0)
         student, _, _ = student_from_teacher(t32, encoder_layers=32, decoder_layers=2)
-        teacher = WhisperForConditionalGeneration(tcfg, dtype=torch.bfloat16, device=device)
-        teacher.store.p16.copy_(t32.store.p16)   # torch_dtype=bf16 teacher (run_distillation.py:1011-1018)
+        teacher = WhisperForConditionalGeneration(tcfg, dtype=tdt, device=device)
+        if tdt == torch.float16:
+            teacher.store.p16.copy_(t32.store.p32)   # torch_dtype=fp16 teacher
+        else:
+            teacher.store.p16.copy_(t32.store.p16)   # torch_dtype=bf16 teacher (run_distillation.py:1011-1018)
         teacher._refresh_ln32()
         del t32
         freeze_encoder = True
     else:
-        teacher = random_init_(WhisperForConditionalGeneration(tcfg, dtype=torch.bfloat16, device=device), seed=0)
+        teacher = random_init_(WhisperForConditionalGeneration(tcfg, dtype=tdt, device=device), seed=0)
         student = random_init_(WhisperForConditionalGeneration(WhisperConfig(**small), dtype=torch.float32,
                                                                device=device), seed=1)
         freeze_encoder = False
+    if args.dtype == "fp16":
+        student.set_compute("fp16")
     torch.cuda.empty_cache()
     return student, teacher, freeze_encoder
 
@@ -415,8 +423,10 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--new-tokens", type=int, default=224, help="c4/c5: new tokens per clip / window")
     ap.add_argument("--seconds", type=float, default=1800.0, help="c5: recording length")
-    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"],
-                    help="c4/c5: model dtype (the reference's decode call sites default to float16)")
+    ap.add_argument("--dtype", default=None, choices=["fp16", "bf16"],
+                    help="c4/c5: model dtype (default fp16: the reference's decode call sites default to float16); "
+                         "c2/c3: the distillation's mixed precision (default bf16: every reference launcher; fp16 = "
+                         "--dtype float16, fp16 autocast + loss scaler)")
     ap.add_argument("--longform-kwargs", default="ref", choices=["ref", "none"],
                     help="c5: run_eval.py:659-665 long-form kwargs (ref) or greedy windows only (none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -426,6 +436,8 @@ def main():
     args.batch = dflt[0] if args.batch is None else args.batch
     args.steps = dflt[1] if args.steps is None else args.steps
     args.warmup = dflt[2] if args.warmup is None else args.warmup
+    if args.dtype is None:
+        args.dtype = "fp16" if args.config in ("c4", "c5") else "bf16"
 
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus is None:
@@ -477,8 +489,9 @@ def main():
 
     def step(i):
         wav, dec, lab = batches[i % len(batches)]
-        _, conv = fe.extract(wav)
-        return trainer.train_step({"conv_input": conv, "decoder_input_ids": dec, "labels": lab})
+        mel, conv = fe.extract(wav)          # fp16: the trainer casts the log-mel into the fp16 conv input itself
+        return trainer.train_step({"conv_input": conv, "input_features": mel, "decoder_input_ids": dec,
+                                   "labels": lab})
 
     for i in range(args.warmup):
         m = step(i)
@@ -514,7 +527,9 @@ def main():
     if not args.no_teacher_fwd:
         # teacher forward (large-v2 encoder + decoder over T_dec 447 + head) ms/clip
         wav, dec, lab = batches[0]
-        _, conv = fe.extract(wav)
+        mel, conv = fe.extract(wav)
+        if args.dtype == "fp16":
+            conv = teacher.conv_input(mel)
         for rep in range(4):
             if rep == 1:
                 torch.cuda.synchronize()
@@ -534,12 +549,13 @@ def main():
         roof = None
         if ks is not None:
             achieved = ks["rate"] / 1e12
-            pmc, pmc_src = load_pmc("gemm_nn") if args.config == "c3" else (None, None)   # the PMC summary is of c3
+            c3b = args.config == "c3" and args.dtype == "bf16"      # the committed PMC summaries are of the bf16 c3 step
+            pmc, pmc_src = load_pmc("gemm_nn") if c3b else (None, None)
             roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=pmc,
                         mfma_busy_frac=(load_mfma("c3_step", "gemm_pp (persistent 256x256 forward GEMM)")
-                                        if args.config == "c3" else None),
-                        kernel="hand-written tw_gemm_bf16 K-major x K-major launches (the forward X.W^T with fused "
+                                        if c3b else None),
+                        kernel=f"hand-written tw_gemm_{args.dtype} K-major x K-major launches (the forward X.W^T with fused "
                                "epilogues: GELU fc1, residual out_proj/fc2 of bf16 streams, long-K fc2): "
                                "gemm_pp_kernel (persistent 256x256 ping-pong, + split-K tail) + "
                                "gemm_kernel<false,false,128,...> for grids under ~1000 256-tiles",
@@ -549,12 +565,12 @@ def main():
                         traffic_over_algo=(round(pmc / ks["avg_bytes"], 3) if pmc and ks["avg_bytes"] else None),
                         # read from committed files, not measured in this run (see each file's `source`)
                         traffic_source=pmc_src,
-                        mfma_busy_source=_committed(MFMA_FILE)[1] if args.config == "c3" else None)
+                        mfma_busy_source=_committed(MFMA_FILE)[1] if c3b else None)
         out = {
             "metric": "distillation utterances/sec (30 s clips)",
             "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (30 s 16 kHz sines + noise, random-init weights, SURVEY.md §8d labels)",
             "config": {"workload": ("c3: distil-32-2 student <- whisper-large-v2 teacher, frozen shared encoder"
                                     if args.config == "c3" else
@@ -573,6 +589,9 @@ def main():
             "final_loss": round(loss, 4),
             "roofline": roof,
             "distributed": dist,
+            # fp16: accelerate's GradScaler state after the timed steps (a skipped step is timed like any other)
+            "loss_scaler": (None if trainer.scaler is None else
+                            {"scale": trainer.scaler.scale, "skipped_steps": trainer.skipped_steps}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

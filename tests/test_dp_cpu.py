@@ -52,6 +52,7 @@ def _worker_allreduce(rank, world, port, out):
     # power-of-two world: the trainer folds 1/world into the loss gradient; otherwise the exchange scales
     st.s.grad = local / world if fold else local.clone()
     st.world, st.pg, st.bucket, st.fold_world, st.dp = world, dist.group.WORLD, 3001, fold, world > 1
+    st.scaler = None
     for name in ("_launch", "launch_grad_exchange", "wait_grad_exchange"):
         setattr(st, name, types.MethodType(getattr(DistillationTrainer, name), st))
     # two "layers" finished during the backward start their exchange early (out of order, uneven
@@ -177,7 +178,7 @@ def _worker_deferred(rank, world, port, out):
     _init(rank, world, port)
     calls = []
     D.F = types.SimpleNamespace(l2norm=lambda g, norm, ws: (calls.append(("norm", g.clone())), norm.fill_(float(g.norm()))),
-                                adamw=lambda p32, g, m, v, p16, lr, b1, b2, eps, wd, t, norm, mx:
+                                adamw=lambda p32, g, m, v, p16, lr, b1, b2, eps, wd, t, norm, mx, inv_scale=1.0:
                                 calls.append(("adamw", lr, t)))
 
     class Stub:
@@ -189,6 +190,7 @@ def _worker_deferred(rank, world, port, out):
     st.s.store.p32 = st.s.store.p16 = torch.zeros(5000)
     st.m_buf, st.v_buf = torch.zeros(5000), torch.zeros(5000)
     st.world, st.pg, st.bucket, st.fold_world, st.dp = world, dist.group.WORLD, 1024, True, world > 1
+    st.scaler = None
     st.norm, st.ws = torch.zeros(1), torch.zeros(8)
     st.runs = [(0, 5000, 0.0)]
     st.lr, st.warmup, st.sched, st.step = 1e-3, 0, "constant", 4
@@ -232,7 +234,7 @@ def _worker_world4(rank, world, port, out):
     D.torch.distributed.all_reduce = rec_ar
     calls = []
     D.F = types.SimpleNamespace(l2norm=lambda g, norm, ws: (calls.append(("norm", g.clone())), norm.fill_(float(g.norm()))),
-                                adamw=lambda p32, g, m, v, p16, lr, b1, b2, eps, wd, t, norm, mx:
+                                adamw=lambda p32, g, m, v, p16, lr, b1, b2, eps, wd, t, norm, mx, inv_scale=1.0:
                                 calls.append(("adamw", lr, t)))
 
     class Stub:
@@ -250,6 +252,7 @@ def _worker_world4(rank, world, port, out):
     st.s.store.p32 = st.s.store.p16 = torch.zeros(n)
     st.m_buf, st.v_buf = torch.zeros(n), torch.zeros(n)
     st.world, st.pg, st.bucket, st.fold_world, st.dp = world, dist.group.WORLD, 2048, True, world > 1
+    st.scaler = None
     st.norm, st.ws = torch.zeros(1), torch.zeros(8)
     st.runs = [(0, n, 0.0)]
     st.lr, st.warmup, st.sched, st.step = 1e-3, 0, "constant", 0

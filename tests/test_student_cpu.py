@@ -126,6 +126,7 @@ def test_run_distillation_mixes_teacher_only(tmp_path):
                                   .view(torch.int16).numpy(), g["mix_bf16_row_u16"])
     np.testing.assert_array_equal(student.state_view("model.decoder.embed_tokens.weight")[SPECIAL["zh"]].numpy(),
                                   st.state_view("model.decoder.embed_tokens.weight")[SPECIAL["zh"]].numpy())
-    args.dtype = "float16"
-    with pytest.raises(NotImplementedError):
-        load_models(args, "cpu")
+    args.dtype = "float16"          # mixed_precision="fp16": fp16 teacher, fp32-master student under fp16 autocast
+    teacher, student = load_models(args, "cpu")
+    assert teacher.dtype == torch.float16 and teacher.compute == "fp16"
+    assert student.dtype == torch.float32 and student.compute == "fp16" and student.store.p16.dtype == torch.float16
