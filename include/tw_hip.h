@@ -91,7 +91,7 @@ int tw_attn_bwd(const void* Q, int64_t ldq, const void* K, int64_t ldk, const vo
 
 /* Fused CE + temperature KL loss and its logits gradient (replaces run_distillation.py:1507-1516,
  * :1539-1549 and HF CE :1082-1087).  out3 = [loss, ce, kl*T^2]; dlogits (same dtype as the logits:
- * bf16 under autocast, fp32 on the fp32 path) may be NULL. */
+ * bf16 under autocast, fp32 on the fp32 path) may be NULL, or s_logits itself (the gradient written in place). */
 int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, int logits_dtype, const int64_t* labels,
              int64_t rows, int V, float T, float ce_w, float kl_w, const int* n_valid, float grad_scale, float* row_out,
              float* out3, void* dlogits, tw_stream_t stream);

@@ -115,12 +115,14 @@ __global__ __launch_bounds__(NT) void klce_kernel(const E* __restrict__ S, const
   const float lse1 = tot.ms + __logf(tot.z1);                // logsumexp(s)
   const float lsesT = tot.ms * invT + __logf(tot.zt);        // logsumexp(s/T)
   const float lsetT = tot.mt * invT + __logf(tot.ztt);       // logsumexp(t/T)
-  const float s_lab = to_f32(srow[lab]);
   if (tid == 0) {
-    row_out[row * 2] = lse1 - s_lab;
+    row_out[row * 2] = lse1 - to_f32(srow[lab]);
     row_out[row * 2 + 1] = (tot.a / tot.ztt) * invT - lsetT + lsesT;
   }
   if (!dS) return;
+  // dS may alias S (the trainer writes the gradient over the student logits, which nothing reads afterwards): every
+  // chunk below is read and then written by the same thread; the barrier orders thread 0's read of s[label] first
+  __syncthreads();
   const float N = (float)max(*n_valid, 1);
   const float gce = grad_scale * ce_w / N;
   const float gkl = grad_scale * kl_w * T / N;
@@ -168,7 +170,7 @@ __global__ void klce_reduce_kernel(const float* __restrict__ row_out, int64_t ro
 
 }  // namespace
 
-// row_out: rows*2 floats workspace; out3: [loss, ce, kl]; dlogits may be null (eval / no grad).
+// row_out: rows*2 floats workspace; out3: [loss, ce, kl]; dlogits may be null (eval / no grad) or s_logits itself.
 extern "C" int tw_kl_ce(const void* s_logits, const void* t_logits, int64_t ld, int logits_dtype,
                         const int64_t* labels, int64_t rows, int V, float T, float ce_w, float kl_w, const int* n_valid,
                         float grad_scale, float* row_out, float* out3, void* dlogits, hipStream_t stream) {

@@ -243,7 +243,7 @@ class DistillationTrainer:
             lt = self._teacher_logits(conv_in, ids, labels, enc16, Tk)
         lab = labels.reshape(-1)
         F.count_valid(lab, self.nvalid)
-        dlogits = torch.empty_like(ls)
+        dlogits = ls      # the loss gradient overwrites the student logits in place (tw_kl_ce): one [B*T, V] block less
         # the loss gradient: 1 / accum (accelerate's backward), the folded DDP mean, and fp16's loss scale
         # (scaler.scale(loss).backward(): the scale enters the fp32 gradient before its fp16 rounding)
         gs = (self.scaler.scale if self.scaler is not None else 1.0) / (self.accum * (self.world if self.fold_world

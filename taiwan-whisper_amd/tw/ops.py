@@ -211,8 +211,9 @@ def kl_ce(s_logits, t_logits, labels, V, n_valid, T=2.0, ce_w=0.8, kl_w=1.0, gra
         row_out = torch.empty(rows * 2, dtype=torch.float32, device=s_logits.device)
     if out3 is None:
         out3 = torch.empty(3, dtype=torch.float32, device=s_logits.device)
-    if dlogits is not None:
+    if dlogits is not None:     # may be s_logits itself (in place)
         assert dlogits.shape == s_logits.shape and dlogits.dtype == s_logits.dtype
+        assert dlogits.data_ptr() != t_logits.data_ptr(), "kl_ce: dlogits may alias the student logits, not the teacher's"
     call("tw_kl_ce", s_logits.data_ptr(), t_logits.data_ptr(), ld, _dt(s_logits), labels.data_ptr(), rows, V, float(T),
          float(ce_w), float(kl_w), n_valid.data_ptr(), float(grad_scale), row_out.data_ptr(), out3.data_ptr(),
          _ptr(dlogits), _stream())

@@ -642,6 +642,10 @@ def test_kl_ce_matches_oracle():
     assert (gd[:, V:] == 0).all()
     assert (gd[::5] == 0).all()
     assert (gd[:, :V] - sl.grad).abs().max() <= 2 ** -7 * sl.grad.abs().max()
+    # in place over the student logits (the trainer's call): the same gradient and losses, bit for bit
+    out3b, _ = ops.kl_ce(sd, td, lab, V, nv, dlogits=sd)
+    torch.cuda.synchronize()
+    assert torch.equal(sd, dl) and torch.equal(out3b, out3)
 
 
 # ----------------------------------------------------------------------------- log-mel
