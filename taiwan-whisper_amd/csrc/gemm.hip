@@ -917,6 +917,42 @@ int launch_dp_tail(const GemmP& p, int m_dp, hipStream_t stream) {
   return 1;
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp16 grids ragged in M or N (the fp16 teacher decoder's M = B x 447 rows, the LM head's N = 51 904): the whole
+// 256x256 tiles [0, Mf) x [0, Nf) on the persistent kernel, the right strip [0, M) x [Nf, N) and the bottom strip
+// [Mf, M) x [0, Nf) on the 128x128 kernel.  Every output keeps the K order of either kernel: bit-identical to the
+// 128x128 kernel alone (tests/test_fp16_train_gpu.py).
+// ---------------------------------------------------------------------------------------------
+template <bool H>
+int launch_pp_edges(const GemmP& p, hipStream_t stream) {
+  const int Mf = p.M / 256 * 256, Nf = p.N / 256 * 256;
+  const int csz = p.c_dtype == TW_BF16 ? 2 : 4, rsz = p.res_dtype == TW_BF16 ? 2 : 4;
+  auto sub = [&](int m0, int n0, int M, int N) {
+    GemmP q = p;
+    q.A = p.A + (int64_t)m0 * p.lda;
+    q.B = p.B + (int64_t)n0 * p.ldb;
+    q.C = (char*)p.C + ((int64_t)m0 * p.ldc + n0) * csz;
+    if (p.bias) q.bias = p.bias + n0;
+    if (p.res) q.res = (const char*)p.res + ((int64_t)m0 * p.ldr + n0) * rsz;
+    if (p.aux) q.aux = p.aux + (int64_t)m0 * p.ldaux + n0;
+    q.M = M;
+    q.N = N;
+    q.epi = pick_epilogue(q, 1);
+    return q;
+  };
+  launch_pp<H>(sub(0, 0, Mf, Nf), 1, stream);
+  TW_CHECK_LAUNCH();
+  if (Nf < p.N) {
+    launch<H, false, false, 128, 128, 2, 2, 2>(sub(0, Nf, p.M, p.N - Nf), 1, stream);
+    TW_CHECK_LAUNCH();
+  }
+  if (Mf < p.M) {
+    launch<H, false, false, 128, 128, 2, 2, 2>(sub(Mf, 0, p.M - Mf, Nf), 1, stream);
+    TW_CHECK_LAUNCH();
+  }
+  return TW_OK;
+}
+
 }  // namespace
 
 // the same per-device block for other stream-ordered scratch users (decode attention split partials)
@@ -997,10 +1033,16 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (flags & 512) tile = 256;
   if (flags & 1024) tile = 2561;      // 256x128, 3-stage ring
   if (flags & 2048) tile = 2562;      // 256x256 ping-pong (K-major A and B only)
-  // the fp16 persistent kernel is compiled with the fast full-tile epilogues only (gemm_impl.h epilogue_k):
-  // ragged shapes and the generic epilogue kind take the 128x128 kernel
-  if (H && tile == 2562 && ((M % 256) || (N % 256) || (K % BK) || p.epi == EPI_GENERIC)) tile = 128;
-  const int64_t ntiles = (tile == 256 || tile == 2562) ? t256 / batch : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  // the fp16 persistent kernel is compiled with the fast full-tile epilogues only (gemm_impl.h epilogue_k): a grid
+  // ragged in M or N runs its whole 256x256 tiles there and the edge strips on the 128x128 kernel (tile 2564,
+  // launch_pp_edges); K tails, batches, row-periodic residuals and the generic epilogue kind take the 128x128 kernel
+  if (H && tile == 2562 && ((M % 256) || (N % 256))) {
+    const bool edges = (K % BK) == 0 && p.epi != EPI_GENERIC && batch == 1 && res_mod == 0 && M >= 256 && N >= 256;
+    tile = edges ? 2564 : 128;
+  }
+  if (H && tile == 2562 && ((K % BK) || p.epi == EPI_GENERIC)) tile = 128;
+  const int64_t ntiles = (tile == 256 || tile == 2562 || tile == 2564) ? t256 / batch
+                                                                       : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (ntiles > 0x7fffffff || ntiles * batch > 0x7fffffff || batch > 65535) return TW_EINVAL;
   // decode-step GEMMs (tools/bench_skinny.py, r01): the weight-streaming kernel wins for N <= 3840
   // (and N <= 8192 at M <= 64); the LM head and wide M=128 GEMMs stream faster as 128x128 tiles
@@ -1083,6 +1125,7 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
   if (tile == 128 && !a_trans && !b_trans && !(flags & 256) &&
       (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch <= pp_grid_cus())
     tile = 1284;
+  if (tile == 2564) return launch_pp_edges<H>(p, stream);
   if (!a_trans && !b_trans) dispatch<H, false, false>(p, batch, stream, tile);
   else if (!a_trans && b_trans) dispatch<H, false, true>(p, batch, stream, tile);
   else if (a_trans && !b_trans) dispatch<H, true, false>(p, batch, stream, tile);

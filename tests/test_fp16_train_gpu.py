@@ -6,7 +6,7 @@ tw_attn_bwd_f16, tw_gelu_bwd_f16, tw_cast_f32_f16, tw_colsum with fp16 rounding,
 GradScaler.unscale_ folded in) -- each against an fp64 / torch reference on the same fp16 inputs, with the
 tolerance stated in the test (one fp16 ulp = 2^-11 relative where an output is rounded to fp16).
 
-Step: tests/golden/cfg_c{1,2,3}.npz rows "f16|..." (tests/golden/make_golden.py gen_cfg_f16): HF Transformers under
+Step: tests/golden/cfg_c{1,2,3,3b10}.npz rows "f16|..." (tests/golden/make_golden.py gen_cfg_f16): HF Transformers under
 torch.autocast(float16) with an fp16 teacher and a default GradScaler (scale 2^16), unscale_ -> clip_grad_norm_ ->
 scaler.step -> scaler.update.  Bars as tests/test_configs_gpu.py with the fixture's own fp16 noise: every tensor
 within 2 x dist(HF fp16, HF fp32) of HF fp16 and 2.5 x of HF fp32 (floors 1e-2 per-tensor norm, 2e-3 total norm),
@@ -82,6 +82,38 @@ def test_gemm_f16_dx_dgelu_epilogue():
     cancel = 1e-6 * (dy.double().abs() @ w.double().abs()) * gp.abs()
     bad = d > 2 ** -9 * ref.abs() + 2 ** -24 + cancel
     assert not bool(bad.any()), (int(bad.sum()), float(d.max()))
+
+
+@pytest.mark.parametrize("M,N,K,flags", [(28608, 5120, 1280, "gelu_aux"), (28608, 1280, 5120, "res32"),
+                                          (28608, 51904, 1280, "store"), (1000, 2560, 1280, "store")])
+def test_gemm_f16_ragged_full_tiles_plus_edges_bit_identical(M, N, K, flags):
+    """fp16 grids ragged in M or N (the fp16 teacher decoder's M = 64 x 447, the LM head's N = 51 904): the whole
+    256x256 tiles on the persistent kernel, the edge strips on the 128x128 kernel -- bit-identical to the 128x128
+    kernel alone (same K order per output)."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A = h(torch.randn(M, K, generator=g)).to(DEV)
+    W = h(torch.randn(N, K, generator=g) * 0.03).to(DEV)
+    bias = h(torch.randn(N, generator=g) * 0.1).to(DEV)
+    outs = []
+    for forced in (0, ops.GEMM_TILE128):
+        kw = {}
+        if flags == "gelu_aux":
+            C = torch.empty(M, N, dtype=torch.float16, device=DEV)
+            kw = dict(aux=torch.empty(M, N, dtype=torch.float16, device=DEV), ldaux=N,
+                      flags=ops.GEMM_ROUND | ops.GEMM_GELU | ops.GEMM_AUX_OUT | forced)
+        elif flags == "res32":
+            C = torch.linspace(-3, 3, M * N, device=DEV).view(M, N).contiguous()
+            kw = dict(res=C, ldr=N, flags=ops.GEMM_ROUND | forced)
+        else:
+            C = torch.empty(M, N, dtype=torch.float16, device=DEV)
+            kw = dict(flags=ops.GEMM_ROUND | forced)
+        ops.gemm(A, W, C, M, N, K, lda=K, ldb=K, ldc=N, bias=bias, **kw)
+        torch.cuda.synchronize()
+        outs.append((C.clone(), kw.get("aux")))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if flags == "gelu_aux":
+        assert torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("N,K,M", [(768, 768, 14304), (264, 136, 4096), (1280, 1280, 1000)])
@@ -247,7 +279,7 @@ def _within_noise(what, got, g, key, dist, floor=0.0, f16_out=False):
     assert d_f32 <= max(2.5 * noise, floor), (what, d_f32, noise)
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c3b10"])   # c3b10: M >= 4096, the production GEMM routes
 def test_fp16_distillation_step_at_baseline_dims(name):
     from tw.distill import DistillationTrainer
     from tw.modeling import to_hf
