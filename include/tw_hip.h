@@ -289,6 +289,9 @@ int tw_attn_bwd_f16(const void* Q, int64_t ldq, const void* K, int64_t ldk, cons
                     float scale, float* workspace, tw_stream_t stream);
 int tw_gelu_bwd_f16(const void* g, int g_dtype, const void* pre, void* out, int64_t n, tw_stream_t stream);
 int tw_cast_f32_f16(const float* src, void* dst, int64_t n, tw_stream_t stream);
+/* tw_add_layernorm_fwd_f16: tw_add_layernorm_fwd on the fp32 stream of fp16 autocast: r and y fp16 (x fp32 only) */
+int tw_add_layernorm_fwd_f16(const void* x, int x_dtype, const void* r, void* x_out, const float* w, const float* b,
+                             void* y, float* mean_out, float* rstd_out, int rows, int D, float eps, tw_stream_t stream);
 int tw_adamw_ex(float* p, const float* g, float* m, float* v, void* p16, int p16_dtype, int64_t n, float lr, float b1,
                 float b2, float eps, float wd, int step, const float* norm, float max_norm, float inv_scale,
                 tw_stream_t stream);

@@ -15,7 +15,8 @@ constexpr int WPB = 4;   // waves (rows) per block
 // epilogue performs, so x_out is bit-identical), then the LayerNorm of x_out.  This moves the fp32
 // residual read + write out of the GEMM epilogue, where every CU of the persistent kernel issues it
 // at once between two tiles, into this streaming pass.
-template <int VEC, int MAXJ, bool ADD = false>
+// RH: r holds fp16 words (the fp16-autocast Linear output), else bf16
+template <int VEC, int MAXJ, bool ADD = false, bool RH = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_dtype,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      void* __restrict__ y, int y_dtype, float* __restrict__ mean_out,
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
       if constexpr (ADD) {
         const f32x4 t = *(const f32x4*)((const float*)x + base + e);
         const bf16x4 u = *(const bf16x4*)(r + base + e);
-        const f32x4 o = f32x4{t[0] + bf2f(u[0]), t[1] + bf2f(u[1]), t[2] + bf2f(u[2]), t[3] + bf2f(u[3])};
+        const f32x4 o = f32x4{t[0] + e2f<RH>(u[0]), t[1] + e2f<RH>(u[1]), t[2] + e2f<RH>(u[2]), t[3] + e2f<RH>(u[3])};
         *(f32x4*)(x_out + base + e) = o;
         v[j][0] = o[0]; v[j][1] = o[1]; v[j][2] = o[2]; v[j][3] = o[3];
       } else if (VEC == 4) {
@@ -388,6 +389,22 @@ extern "C" int tw_add_layernorm_fwd(const void* x, int x_dtype, const void* r, v
                                   rows, D, eps, rb, xo); break;
     }
   }
+  TW_CHECK_LAUNCH();
+  return TW_OK;
+}
+
+// fp16 autocast (round 6): x_out = x + r over the fp32 stream with r the fp16 Linear output, y = fp16 LN(x_out)
+extern "C" int tw_add_layernorm_fwd_f16(const void* x, int x_dtype, const void* r, void* x_out, const float* w,
+                                        const float* b, void* y, float* mean_out, float* rstd_out, int rows, int D,
+                                        float eps, hipStream_t stream) {
+  if (rows <= 0) return TW_OK;
+  if (D % 256 || D > 1280) return TW_EUNSUPPORTED;
+  if (x_dtype != TW_F32) return TW_EUNSUPPORTED;
+  if ((((uintptr_t)x | (uintptr_t)r | (uintptr_t)x_out | (uintptr_t)y | (uintptr_t)w | (uintptr_t)b) & 15) != 0)
+    return TW_EINVAL;
+  hipLaunchKernelGGL((ln_fwd_kernel<4, 5, true, true>), dim3((rows + WPB - 1) / WPB), dim3(64 * WPB), 0, stream, x,
+                     (int)TW_F32, w, b, y, (int)TW_F16, mean_out, rstd_out, rows, D, eps, (const bf16*)r,
+                     (float*)x_out);
   TW_CHECK_LAUNCH();
   return TW_OK;
 }

@@ -68,6 +68,7 @@ SIGNATURES = {
                         I32, I32, F32, P, P],
     "tw_gelu_bwd_f16": [P, I32, P, P, I64, P],
     "tw_cast_f32_f16": [P, P, I64, P],
+    "tw_add_layernorm_fwd_f16": [P, I32, P, P, P, P, P, P, P, I32, I32, F32, P],
     "tw_adamw_ex": [P, P, P, P, P, I32, I64, F32, F32, F32, F32, F32, I32, P, F32, F32, P],
     # fp32 arithmetic path
     "tw_gemm_f32": [P, I64, I32, P, I64, I32, P, I64, I32, I32, I32, I32, I64, I64, I64, I32, I64, I64, I64, F32,

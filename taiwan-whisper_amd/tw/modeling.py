@@ -463,8 +463,12 @@ class WhisperForConditionalGeneration:
         the bf16 teacher stream for out_proj only (the plain-bias projection then runs the store-only epilogue; at
         fc2 the extra LN traffic costs what the epilogue saves).  DESIGN.md §5; TW_DEFER_RES=0 disables (A/B runs)."""
         # tw_add_layernorm_fwd: D % 256 == 0 and D <= 1280 (every Whisper size), else the residual epilogue
-        if _DEFER_RES == "0" or self.act_dtype != torch.bfloat16 or self.config.d_model % 256 or self.config.d_model > 1280:
+        if _DEFER_RES == "0" or self.act_dtype == torch.float32 or self.config.d_model % 256 or self.config.d_model > 1280:
             return False
+        if self.act_dtype == torch.float16:
+            # fp16 autocast's fp32 stream (tw_add_layernorm_fwd_f16); the fp16 model's fp16 stream keeps the residual
+            # epilogue, which also applies the encoder's fp16 clamp
+            return self.stream_dtype == torch.float32
         return self.stream_dtype == torch.float32 or (kind == "attn" and _DEFER_RES != "2")
 
     def _ln_in(self, x, pend, name, save):

@@ -141,17 +141,20 @@ def layernorm_fwd(x, w, b, y, mean=None, rstd=None, eps=1e-5):
 
 
 def add_layernorm_fwd(x, r, x_out, w, b, y, mean=None, rstd=None, eps=1e-5):
-    """x_out = x + r (fp32 or bf16 residual stream + the preceding Linear's bf16 output), y = bf16 LN(x_out)."""
+    """x_out = x + r (fp32 or bf16 residual stream + the preceding Linear's bf16 output), y = bf16 LN(x_out); fp16
+    autocast: fp32 stream, r and y fp16 (tw_add_layernorm_fwd_f16)."""
     D = x.shape[-1]
     rows = x.numel() // D
-    assert x.dtype in (torch.float32, torch.bfloat16) and x_out.dtype == x.dtype and r.dtype == torch.bfloat16
-    assert y.dtype == torch.bfloat16
+    h = r.dtype
+    assert h in HALF and y.dtype == h and x_out.dtype == x.dtype
+    assert x.dtype in ((torch.float32, torch.bfloat16) if h == torch.bfloat16 else (torch.float32,))
     for t in (x, r, x_out, y):
         assert t.is_contiguous() and t.numel() == x.numel() and t.is_cuda
     assert w.dtype == torch.float32 and b.dtype == torch.float32 and w.numel() == D and b.numel() == D
     if mean is not None:
         _need(mean, rows, "ln mean"); _need(rstd, rows, "ln rstd")
-    call("tw_add_layernorm_fwd", x.data_ptr(), _dt(x), r.data_ptr(), x_out.data_ptr(), w.data_ptr(), b.data_ptr(),
+    call("tw_add_layernorm_fwd_f16" if h == torch.float16 else "tw_add_layernorm_fwd", x.data_ptr(), _dt(x),
+         r.data_ptr(), x_out.data_ptr(), w.data_ptr(), b.data_ptr(),
          y.data_ptr(), _ptr(mean), _ptr(rstd), rows, D, float(eps), _stream())
     return y
 

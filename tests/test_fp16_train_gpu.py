@@ -116,6 +116,35 @@ def test_gemm_f16_ragged_full_tiles_plus_edges_bit_identical(M, N, K, flags):
         assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("D", [768, 1280])
+def test_add_layernorm_f16_matches_residual_epilogue(D):
+    """fp16 autocast's deferred residual update (fp32 stream + fp16 Linear output r, then the LayerNorm with fp16
+    output: tw_add_layernorm_fwd_f16) == the fp16 GEMM's fp32 residual epilogue followed by tw_layernorm_fwd, bit for
+    bit, in place and into a separate stream buffer."""
+    from tw import ops
+    g = torch.Generator().manual_seed(D + 7)
+    rows, K = 1000, 256
+    x0 = (torch.randn(rows, D, generator=g) * 3).to(DEV)
+    A, W = h(torch.randn(rows, K, generator=g)).to(DEV), h(torch.randn(D, K, generator=g) * 0.1).to(DEV)
+    bias = h(torch.randn(D, generator=g)).to(DEV)
+    w, b = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    xa = x0.clone()
+    ops.gemm(A, W, xa, rows, D, K, lda=K, ldb=K, ldc=D, bias=bias, res=xa, ldr=D, flags=ops.GEMM_ROUND)
+    ya = torch.empty(rows, D, dtype=torch.float16, device=DEV)
+    ma, ra = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(xa, w, b, ya, ma, ra)
+    r = torch.empty(rows, D, dtype=torch.float16, device=DEV)
+    ops.gemm(A, W, r, rows, D, K, lda=K, ldb=K, ldc=D, bias=bias, flags=ops.GEMM_ROUND)
+    for inplace in (True, False):
+        xb = x0.clone()
+        xo = xb if inplace else torch.empty_like(xb)
+        yb = torch.empty_like(ya)
+        mb, rb = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+        ops.add_layernorm_fwd(xb, r, xo, w, b, yb, mb, rb)
+        torch.cuda.synchronize()
+        assert torch.equal(xo, xa) and torch.equal(yb, ya) and torch.equal(mb, ma) and torch.equal(rb, ra)
+
+
 @pytest.mark.parametrize("N,K,M", [(768, 768, 14304), (264, 136, 4096), (1280, 1280, 1000)])
 def test_gemm_f16_splitk_weight_grad(N, K, M):
     """dW += fp16(dY^T X) through the split-K path vs the unsplit kernel: one fp16 ulp of the product plus the fp32
