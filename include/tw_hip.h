@@ -124,7 +124,7 @@ int tw_transpose_bf16(const void* src, int64_t ld_src, int rows, int cols, void*
 /* autocast weight cast fp32 -> bf16 (ACC:accelerator.py autocast of every Linear weight). */
 int tw_cast_f32_bf16(const float* src, void* dst, int64_t n, tw_stream_t stream);
 /* bias gradient: out[c] (+)= [round](sum_r x[r][c]) (round_bf16: 0 none, 1 to bf16, 2 to fp16; x fp32 / bf16 / fp16);
- * deterministic two-pass, workspace >= ceil(rows/256)*cols. */
+ * deterministic two-pass, workspace >= ceil(rows/64)*cols. */
 int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum, int round_bf16,
               float* workspace, int64_t workspace_floats, tw_stream_t stream);
 

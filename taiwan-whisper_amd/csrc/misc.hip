@@ -36,9 +36,11 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __rest
 }
 
 // Column sums over rows (bias gradient of an autocast Linear, computed in bf16 then added to the
-// fp32 grad).  Pass 1: block (ROWS_PER x 512 columns) -> partial[chunk][cols] with 8 columns per
+// fp32 grad).  Pass 1: block (CS_ROWS x 512 columns) -> partial[chunk][cols] with 8 columns per
 // lane (16-B bf16 / 2x16-B fp32 loads); pass 2: deterministic sum over chunks (+round, +accumulate).
-constexpr int CS_COLS = 512, CS_ROWS = 256;
+// 64-row chunks (round 6; were 256): c2's decoder bias gradients (14 304 rows x 768) ran on 112 blocks at 0.8 TB/s
+// and the encoder's (48 000 rows) on 376 at 1.9 TB/s -- too few loads in flight for HBM.
+constexpr int CS_COLS = 512, CS_ROWS = 64;
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restrict__ x, int x_dtype, int64_t ldx,
                                                              int rows, int cols, float* __restrict__ partial) {
   __shared__ float red[4][CS_COLS];
@@ -48,6 +50,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restr
   const int r1 = min(rows, r0 + CS_ROWS);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const bool vec = (c0 + 7 < cols) && ((ldx & 7) == 0);
+#pragma unroll 4
   for (int r = r0 + wv; r < r1; r += 4) {
     const int64_t o = (int64_t)r * ldx + c0;
     if (vec) {
@@ -80,20 +83,21 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restr
   }
 }
 
-// out[c] = [out[c] +] round?(sum_k partial[k][c]) (round 1: to bf16, 2: to fp16): 64 columns per block, 16 thread rows each
-// summing every 16th chunk, fixed-order combine in LDS (deterministic)
+// out[c] = [out[c] +] round?(sum_k partial[k][c]) (round 1: to bf16, 2: to fp16): 16 columns per block, 64 thread
+// rows each summing every 64th chunk, fixed-order combine in LDS (deterministic)
 __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ partial, int nchunk, int cols,
                                                             float* __restrict__ out, int accum, int round_bf16) {
-  __shared__ float st[16][64];
-  const int cl = threadIdx.x & 63, j = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float st[64][16];
+  const int cl = threadIdx.x & 15, j = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float t = 0.f;
   if (c < cols)
-    for (int k = j; k < nchunk; k += 16) t += partial[(int64_t)k * cols + c];
+#pragma unroll 4
+    for (int k = j; k < nchunk; k += 64) t += partial[(int64_t)k * cols + c];
   st[j][cl] = t;
   __syncthreads();
   if (j == 0 && c < cols) {
-    for (int k = 1; k < 16; ++k) t += st[k][cl];
+    for (int k = 1; k < 64; ++k) t += st[k][cl];
     if (round_bf16 == 2) t = rnd<true>(t);
     else if (round_bf16) t = rbf(t);
     out[c] = accum ? out[c] + t : t;
@@ -311,7 +315,7 @@ extern "C" int tw_cast_f32_f16(const float* src, void* dst, int64_t n, hipStream
   return TW_OK;
 }
 
-// workspace >= ceil(rows/256) * cols floats
+// workspace >= ceil(rows/64) * cols floats
 extern "C" int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int cols, float* out, int accum,
                          int round_bf16, float* workspace, int64_t workspace_floats, hipStream_t stream) {
   if (rows <= 0 || cols <= 0) return TW_OK;
@@ -319,7 +323,7 @@ extern "C" int tw_colsum(const void* x, int x_dtype, int64_t ldx, int rows, int 
   if (workspace_floats < (int64_t)nchunk * cols) return TW_EINVAL;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + CS_COLS - 1) / CS_COLS, nchunk), dim3(256), 0, stream, x,
                      x_dtype, ldx, rows, cols, workspace);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64), dim3(1024), 0, stream, workspace, nchunk, cols, out,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 15) / 16), dim3(1024), 0, stream, workspace, nchunk, cols, out,
                      accum, round_bf16);
   TW_CHECK_LAUNCH();
   return TW_OK;

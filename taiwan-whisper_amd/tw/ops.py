@@ -311,7 +311,7 @@ def colsum(x, ldx, rows, cols, out, accum=True, round_bf16=True):
     """out (+)= [round](column sums of x); round_bf16: False / True (bf16) / 2 (fp16)."""
     _need(x, (rows - 1) * ldx + cols, "colsum x")
     assert out.dtype == torch.float32 and out.numel() >= cols
-    n = (rows + 255) // 256 * cols
+    n = (rows + 63) // 64 * cols           # one fp32 partial row per 64-row chunk (tw_colsum)
     ws = workspace(n, x.device, "colsum")
     call("tw_colsum", x.data_ptr(), _dt(x), ldx, rows, cols, out.data_ptr(), int(accum), int(round_bf16),
          ws.data_ptr(), ws.numel(), _stream())
