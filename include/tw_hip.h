@@ -78,6 +78,11 @@ int tw_add_layernorm_fwd(const void* x, int x_dtype, const void* r, void* x_out,
 int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd, const void* dy,
                      int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out, int rows, int D,
                      float* workspace, int64_t workspace_floats, tw_stream_t stream);
+/* tw_layernorm_bwd_ex: tw_layernorm_bwd that also writes g16 = the bf16 (g_dtype 1) / fp16 (2) rounding of the final dx
+ * (the autocast cast of the stream gradient the preceding block's GEMMs read; g16 may be NULL). */
+int tw_layernorm_bwd_ex(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd, const void* dy,
+                        int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out, int rows, int D,
+                        float* workspace, int64_t workspace_floats, void* g16, int g_dtype, tw_stream_t stream);
 
 /* Flash attention, head_dim 64, bf16 (replaces SDPA at HF modeling_whisper.py:337-350 for encoder
  * self-attn, decoder causal self-attn and cross-attn).  lse: [B][H][Tq] fp32 (natural log). */

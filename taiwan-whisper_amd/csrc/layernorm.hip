@@ -185,12 +185,15 @@ __device__ __forceinline__ f32x4 ld4_as_f32(const void* p, int dtype, int64_t i)
 
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)); dx accumulated into dx_out (fp32).
 // Per-block partial dw/db written to partial[blockIdx.x][2][D] for a column reduction.
+// g16 (optional): the 16-bit copy of the final dx (g_dtype 1 bf16, 2 fp16) -- the autocast rounding of the stream
+// gradient that the preceding block's first GEMM consumes, fused here instead of a separate cast pass.
 template <int VEC, int MAXJ>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x, int x_dtype,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const void* __restrict__ dy,
                                                      int dy_dtype, float* __restrict__ dx, int dx_accum,
-                                                     float* __restrict__ partial, int rows, int D) {
+                                                     float* __restrict__ partial, int rows, int D,
+                                                     void* __restrict__ g16 = nullptr, int g_dtype = TW_BF16) {
   __shared__ float red[WPB][2][1280];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
@@ -255,12 +258,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x,
           for (int q = 0; q < 4; ++q) o[q] = rs * (g[j][q] - s1 - xh[j][q] * s2);
           if (dx_accum) o += *(const f32x4*)d;
           *(f32x4*)d = o;
+          if (g16) {
+            const int64_t e = base + (j * 64 + lane) * 4;
+            if (g_dtype == TW_F16)
+              *(f16x4*)((f16*)g16 + e) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+            else
+              *(bf16x4*)((bf16*)g16 + e) = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+          }
         } else {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) {
             const int e = (j * 64 + lane) * VEC + q;
             const float o = rs * (g[j][q] - s1 - xh[j][q] * s2);
-            if (dx_accum) dx[base + e] += o; else dx[base + e] = o;
+            const float f = dx_accum ? dx[base + e] + o : o;
+            dx[base + e] = f;
+            if (g16) st_from_f32(g16, g_dtype, base + e, f);
           }
         }
       }
@@ -409,21 +421,24 @@ extern "C" int tw_add_layernorm_fwd_f16(const void* x, int x_dtype, const void* 
   return TW_OK;
 }
 
-// workspace: >= nblk*2*D floats where nblk = min(1024, ceil(rows/4)); dw/db accumulated into dw_out/db_out
-extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd,
-                                const void* dy, int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out,
-                                int rows, int D, float* workspace, int64_t workspace_floats, hipStream_t stream) {
+// workspace: >= nblk*2*D floats where nblk = min(1024, ceil(rows/4)); dw/db accumulated into dw_out/db_out;
+// g16 (may be NULL): also the bf16 (g_dtype 1) / fp16 (2) rounding of the final dx
+extern "C" int tw_layernorm_bwd_ex(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd,
+                                   const void* dy, int dy_dtype, float* dx, int dx_accum, float* dw_out,
+                                   float* db_out, int rows, int D, float* workspace, int64_t workspace_floats,
+                                   void* g16, int g_dtype, hipStream_t stream) {
   if (rows <= 0) return TW_OK;
+  if (g16 && g_dtype != TW_BF16 && g_dtype != TW_F16) return TW_EINVAL;
   if (D % 64 || D > 1280) return TW_EUNSUPPORTED;
   int nblk = (rows + WPB - 1) / WPB;
   if (nblk > 1024) nblk = 1024;
   if (workspace_floats < (int64_t)nblk * 2 * D) return TW_EINVAL;
   // VEC 4 with the exact number of 256-column chunks as MAXJ: the per-lane arrays (x, dy, xhat, g, dw, db) sized
   // for the row, not for D = 1280 (D = 768: fewer registers, more waves per SIMD)
-  const bool v4 = D % 256 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w) & 15) == 0;
+  const bool v4 = D % 256 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w | (uintptr_t)g16) & 15) == 0;
 #define TW_LN_BWD(J)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_kernel<4, J>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy, dy_dtype, \
-                     dx, dx_accum, workspace, rows, D)
+                     dx, dx_accum, workspace, rows, D, g16, g_dtype)
   // D = 1280 holds 162 VGPRs = 3 waves per SIMD: one block per resident slot (768 on a 256-CU MI355X: all resident
   // at once) instead of a 1024-block grid whose last quarter would run as a second, mostly idle round.  The cap is
   // the occupancy query x the device's CU count (cached), not a constant of one part.
@@ -445,10 +460,17 @@ extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, cons
 #undef TW_LN_BWD
   else
     hipLaunchKernelGGL((ln_bwd_kernel<1, 20>), dim3(nblk), dim3(256), 0, stream, x, x_dtype, w, mean, rstd, dy,
-                       dy_dtype, dx, dx_accum, workspace, rows, D);
+                       dy_dtype, dx, dx_accum, workspace, rows, D, g16, g_dtype);
   TW_CHECK_LAUNCH();
   hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((D + 63) / 64), dim3(1024), 0, stream, workspace, nblk, D, dw_out,
                      db_out);
   TW_CHECK_LAUNCH();
   return TW_OK;
+}
+
+extern "C" int tw_layernorm_bwd(const void* x, int x_dtype, const float* w, const float* mean, const float* rstd,
+                                const void* dy, int dy_dtype, float* dx, int dx_accum, float* dw_out, float* db_out,
+                                int rows, int D, float* workspace, int64_t workspace_floats, hipStream_t stream) {
+  return tw_layernorm_bwd_ex(x, x_dtype, w, mean, rstd, dy, dy_dtype, dx, dx_accum, dw_out, db_out, rows, D, workspace,
+                             workspace_floats, nullptr, TW_BF16, stream);
 }

@@ -24,6 +24,7 @@ SIGNATURES = {
                      P, I64, I64, I32, P, P],
     "tw_layernorm_fwd": [P, I32, P, P, P, I32, P, P, I32, I32, F32, P],
     "tw_layernorm_bwd": [P, I32, P, P, P, P, I32, P, I32, P, P, I32, I32, P, I64, P],
+    "tw_layernorm_bwd_ex": [P, I32, P, P, P, P, I32, P, I32, P, P, I32, I32, P, I64, P, I32, P],
     "tw_add_layernorm_fwd": [P, I32, P, P, P, P, P, P, P, I32, I32, F32, P],
     "tw_attn_fwd": [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, F32, P],
     "tw_attn_bwd": [P, I64, P, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, I32, I32, I32, I32,

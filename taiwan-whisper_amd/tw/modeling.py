@@ -35,6 +35,7 @@ from . import ops
 from .config import GenerationConfig, WhisperConfig
 
 _DEFER_RES = os.environ.get("TW_DEFER_RES", "1")   # "0": never, "2": fp32 streams only, else default
+_LN_G16 = os.environ.get("TW_LN_G16", "1") != "0"  # "0": the backward casts the stream gradient separately (A/B runs)
 
 F = ops
 
@@ -715,6 +716,9 @@ class Backward:
         # "model.decoder.layers.1.") is final, so the DP exchange of that range can start while the
         # rest of the backward runs
         self.on_ready = None
+        # (dx, g): the 16-bit copy of the stream gradient dx written by the LayerNorm backward that produced dx's
+        # current value (the autocast cast the next block's GEMMs read), taken by _grad16
+        self._g16 = None
 
     def _layer_done(self, p):
         if self.on_ready is not None and p.endswith(".self_attn"):
@@ -756,14 +760,25 @@ class Backward:
                  round_bf16={"fp32": 0, "fp16": 2}.get(self.m.compute, 1))
 
     def ln(self, sv, name, dy, dx):
+        """dx += LayerNorm backward; on the 16-bit paths the kernel also writes dx's autocast rounding (_grad16)."""
         x, mean, rstd, _ = sv[name]
         m = self.m
         D = x.shape[-1]
         need = min(1024, (x.shape[0] + 3) // 4) * 2 * D
         if self._ln_ws is None or self._ln_ws.numel() < need:
             self._ln_ws = torch.empty(need, dtype=torch.float32, device=self.dev)
+        g16 = torch.empty(dx.shape, dtype=m.act_dtype, device=self.dev) if m.compute != "fp32" and _LN_G16 else None
         F.layernorm_bwd(x, m.ln_param(name + ".weight"), mean, rstd, dy, dx, m.gv(name + ".weight"),
-                        m.gv(name + ".bias"), dx_accum=True, workspace=self._ln_ws)
+                        m.gv(name + ".bias"), dx_accum=True, workspace=self._ln_ws, g16=g16)
+        self._g16 = (dx, g16) if g16 is not None else None
+
+    def _grad16(self, dx):
+        """The stream gradient as the block's GEMMs read it (m.act_grad(dx)): the LayerNorm backward's fused copy when it
+        wrote dx's current value, else a cast."""
+        c, self._g16 = self._g16, None
+        if c is not None and c[0] is dx:
+            return c[1]
+        return self.m.act_grad(dx)
 
     def span_grad(self, first, last, shape):
         m = self.m
@@ -774,7 +789,7 @@ class Backward:
     # ------------------------------------------------------------------
     def mlp(self, p, st, dx):
         m = self.m
-        g = m.act_grad(dx)
+        g = self._grad16(dx)
         M = g.shape[0]
         self.dW(g, st["h"], m.gv(p + ".fc2.weight"), M)
         self.db(g, (0, g.shape[1]), m.gv(p + ".fc2.bias"))
@@ -793,7 +808,7 @@ class Backward:
         H = d // 64
         B, T = st["B"], st["T"]
         M = B * T
-        g = m.act_grad(dx)
+        g = self._grad16(dx)
         self.dW(g, st["o"], m.gv(p + ".out_proj.weight"), M)
         self.db(g, (0, d), m.gv(p + ".out_proj.bias"))
         do = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)
@@ -816,7 +831,7 @@ class Backward:
         H = d // 64
         B, T, Tk = st["B"], st["T"], st["Tk"]
         M = B * T
-        g = m.act_grad(dx)
+        g = self._grad16(dx)
         self.dW(g, st["o"], m.gv(p + ".out_proj.weight"), M)
         self.db(g, (0, d), m.gv(p + ".out_proj.bias"))
         do = torch.empty(M, d, dtype=m.act_dtype, device=self.dev)

@@ -159,16 +159,23 @@ def add_layernorm_fwd(x, r, x_out, w, b, y, mean=None, rstd=None, eps=1e-5):
     return y
 
 
-def layernorm_bwd(x, w, mean, rstd, dy, dx, dw, db, dx_accum=True, workspace=None):
+def layernorm_bwd(x, w, mean, rstd, dy, dx, dw, db, dx_accum=True, workspace=None, g16=None):
+    """dx (+)= LayerNorm backward; g16 (optional, bf16 / fp16, dx's shape): the 16-bit rounding of the final dx."""
     D = x.shape[-1]
     rows = x.numel() // D
     assert dx.dtype == torch.float32 and dx.numel() == x.numel() and dy.numel() == x.numel()
     nblk = min(1024, (rows + 3) // 4)
     if workspace is None or workspace.numel() < nblk * 2 * D:
         workspace = torch.empty(nblk * 2 * D, dtype=torch.float32, device=x.device)
-    call("tw_layernorm_bwd", x.data_ptr(), _dt(x), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
-         _dt(dy), dx.data_ptr(), int(dx_accum), _ptr(dw), _ptr(db), rows, D, workspace.data_ptr(),
-         workspace.numel(), _stream())
+    if g16 is None:
+        call("tw_layernorm_bwd", x.data_ptr(), _dt(x), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
+             _dt(dy), dx.data_ptr(), int(dx_accum), _ptr(dw), _ptr(db), rows, D, workspace.data_ptr(),
+             workspace.numel(), _stream())
+        return dx
+    assert g16.dtype in HALF and g16.is_contiguous() and g16.numel() == dx.numel() and dx.is_contiguous()
+    call("tw_layernorm_bwd_ex", x.data_ptr(), _dt(x), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
+         _dt(dy), dx.data_ptr(), int(dx_accum), _ptr(dw), _ptr(db), rows, D, workspace.data_ptr(), workspace.numel(),
+         g16.data_ptr(), _dt(g16), _stream())
     return dx
 
 
