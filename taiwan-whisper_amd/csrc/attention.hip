@@ -82,7 +82,7 @@ __device__ __forceinline__ bf16x8 pack8e(const f32x4& a, const f32x4& b) {
 
 struct AttnP {
   const bf16* Q; const bf16* K; const bf16* V; bf16* O; float* lse;
-  const bf16* dO; const float* Dv; bf16* dQ; bf16* dK; bf16* dV;
+  const bf16* dO; float* Dv; bf16* dQ; bf16* dK; bf16* dV;
   int64_t ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
   int B, H, Tq, Tk, causal;
   float scale, scale_log2;
@@ -292,24 +292,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP p) {
 
 
 // ------------------------------------------------------------------------------------
-// D[b,h,q] = sum_e dO[q][e] * O[q][e]     (one wave per (row, head))
-template <bool F16>
-__global__ void attn_bwd_pre_kernel(const bf16* __restrict__ dO, int64_t lddo, const bf16* __restrict__ O,
-                                    int64_t ldo, float* __restrict__ Dv, int B, int H, int Tq) {
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= (int64_t)B * Tq * H) return;
-  const int lane = lane_id();
-  const int h = w % H;
-  const int64_t row = w / H;   // b*Tq + q
-  const float v = e2f<F16>(dO[row * lddo + h * 64 + lane]) * e2f<F16>(O[row * ldo + h * 64 + lane]);
-  const float s = wave_sum_dpp(v);
-  if (lane == 0) {
-    const int b = row / Tq, q = row % Tq;
-    Dv[((int64_t)b * H + h) * Tq + q] = s;
-  }
-}
-
-// dQ: per query block, loop over key tiles (K, V in LDS)
+// dQ: per query block, loop over key tiles (K, V in LDS).  Also computes D[q] = sum_e dO[q][e] O[q][e] for its rows
+// (each lane's 16 products, then the 4 lanes of a row by xor-16 / xor-32 swaps) and stores it for the dK/dV kernel,
+// which runs after it: no separate pass over dO and O.
 template <bool H>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];
@@ -326,18 +311,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
   const bf16* Vb = p.V + (int64_t)b * p.Tk * p.ldv + h * 64;
   const int off = p.Tk - p.Tq;
 
+  const bf16* Ob = p.O + (int64_t)b * p.Tq * p.ldo + h * 64;
   bf16x8 qf[2][2], dof[2][2];
   float lse2[2], Dq[2];
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
     const int q = qw + qi * 16 + li;
+    float dd = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       qf[qi][kk] = ld_frag(Qb, p.ldq, q, p.Tq, kk, lane);
       dof[qi][kk] = ld_frag(dOb, p.lddo, q, p.Tq, kk, lane);
+      const bf16x8 of = ld_frag(Ob, p.ldo, q, p.Tq, kk, lane);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dd += e2f<H>(dof[qi][kk][e]) * e2f<H>(of[e]);
     }
     lse2[qi] = q < p.Tq ? p.lse[(int64_t)bh * p.Tq + q] * LOG2E : 0.f;
-    Dq[qi] = q < p.Tq ? p.Dv[(int64_t)bh * p.Tq + q] : 0.f;
+    Dq[qi] = swap32_sum(swap16_sum(dd));                 // rows past Tq: zero fragments, D = 0
+    if (g == 0 && q < p.Tq) p.Dv[(int64_t)bh * p.Tq + q] = Dq[qi];
   }
   f32x4 dq[4][2];
 #pragma unroll
@@ -391,7 +382,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) {
           const int key = k0 + kj * 16 + 4 * g + r;
           const bool ok = !need_mask || (key < p.Tk && q < p.Tq && (!p.causal || key <= q + off));
-          const float pr = ok ? __builtin_amdgcn_exp2f(s[kj][qi][r] * p.scale_log2 - lse2[qi]) : 0.f;
+          // masked scores as exp2(-inf) = 0: a select, not a branch per element (interior tiles: ok is always true)
+          const float pr = __builtin_amdgcn_exp2f(ok ? s[kj][qi][r] * p.scale_log2 - lse2[qi] : -INFINITY);
           s[kj][qi][r] = pr * (dp[kj][qi][r] - Dq[qi]);   // dS^T
         }
     }
@@ -516,7 +508,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnP p) {
         for (int kj = 0; kj < 2; ++kj) {
           const int key = kw + kj * 16 + li;
           const bool ok = !need_mask || (q < p.Tq && key < p.Tk && (!p.causal || key <= q + off));
-          const float pr = ok ? __builtin_amdgcn_exp2f(s[qf][kj][r] * p.scale_log2 - l2) : 0.f;
+          const float pr = __builtin_amdgcn_exp2f(ok ? s[qf][kj][r] * p.scale_log2 - l2 : -INFINITY);   // select, no branch
           s[qf][kj][r] = pr;                              // P
           dp[qf][kj][r] = pr * (dp[qf][kj][r] - Dq);      // dS
         }
@@ -609,23 +601,20 @@ int attn_bwd_run(const void* Q, int64_t ldq, const void* K, int64_t ldk, const v
                  float scale, float* workspace, bool half, hipStream_t stream) {
   if (head_dim != 64) return TW_EUNSUPPORTED;
   if (B <= 0 || Tq <= 0 || Tk <= 0) return TW_OK;
-  if (!check_common(Q, K, V, ldq, ldk, ldv) || ((uintptr_t)dO & 15) || (lddo & 7)) return TW_EINVAL;
+  if (!check_common(Q, K, V, ldq, ldk, ldv) || ((uintptr_t)dO & 15) || (lddo & 7) || ((uintptr_t)O & 15) || (ldo & 7))
+    return TW_EINVAL;
   if (causal && Tq > Tk) return TW_EINVAL;
   AttnP p = {};
-  p.Q = (const bf16*)Q; p.K = (const bf16*)K; p.V = (const bf16*)V; p.lse = (float*)lse;
+  p.Q = (const bf16*)Q; p.K = (const bf16*)K; p.V = (const bf16*)V; p.lse = (float*)lse; p.O = (bf16*)O;
   p.dO = (const bf16*)dO; p.Dv = workspace; p.dQ = (bf16*)dQ; p.dK = (bf16*)dK; p.dV = (bf16*)dV;
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo; p.lddo = lddo; p.lddq = lddq; p.lddk = lddk; p.lddv = lddv;
   p.B = B; p.H = H; p.Tq = Tq; p.Tk = Tk; p.causal = causal;
   p.scale = scale; p.scale_log2 = scale * LOG2E;
-  const int64_t nw = (int64_t)B * Tq * H;
+  // dQ (and D, which the dK/dV kernel reads) first, then dK/dV
   if (half) {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<true>, dim3((nw + 3) / 4), dim3(256), 0, stream, (const bf16*)dO, lddo,
-                       (const bf16*)O, ldo, workspace, B, H, Tq);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, dim3((Tk + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   } else {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<false>, dim3((nw + 3) / 4), dim3(256), 0, stream, (const bf16*)dO, lddo,
-                       (const bf16*)O, ldo, workspace, B, H, Tq);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, dim3((Tq + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3((Tk + QB - 1) / QB, B * H), dim3(256), 0, stream, p);
   }
