@@ -125,7 +125,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_kernel(GemmP p) {
     __builtin_amdgcn_s_barrier();
   }
 
-  epilogue<H, BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, lane, bz);
+  epilogue<H, BM, BN, WM, WN, 0, -1, BT && !AT>(p, acc, m0, n0, wm, wn, lane, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -632,6 +632,9 @@ int pick_epilogue(const GemmP& p, int batch) {
     const bool x8 = (p.ldaux % 8) == 0 && (batch == 1 || (p.sAux % 8) == 0) && a16(p.aux);
     return x8 ? EPI_GELU_AUX : EPI_GENERIC;
   }
+  if (f == (F_ROUND | F_DGELU) && p.c_dtype == TW_BF16 && c8 && (p.ldaux % 8) == 0 &&
+      (batch == 1 || (p.sAux % 8) == 0) && a16(p.aux))
+    return EPI_DGELU;             // (the dX kernels: gemm_kernel's epilogue<..., DG>; elsewhere the generic form)
   if ((f & ~(F_BIAS | F_ROUND | F_CLAMP16)) == F_RES && p.res_mod == 0 && p.res_dtype == p.c_dtype) {
     if (p.c_dtype == TW_BF16 && c8 && (p.ldr % 8) == 0 && (batch == 1 || (p.sR % 8) == 0) && a16(p.res))
       return EPI_RES_BF16;

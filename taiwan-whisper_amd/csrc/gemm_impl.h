@@ -301,7 +301,8 @@ __device__ __forceinline__ void epilogue_generic(const GemmP& p, const f32x4 (&a
 // to fragment order (the swap is an involution), so each lane reads and writes the same bytes
 // (in-place residual updates stay race-free).
 // ---------------------------------------------------------------------------------------------
-enum { EPI_GENERIC = 0, EPI_STORE_BF16, EPI_STORE_F32, EPI_GELU, EPI_GELU_AUX, EPI_RES_BF16, EPI_RES_F32 };
+// EPI_DGELU (round 6): the GELU backward of the dX products, v = e(e(acc) * gelu'(aux)) on 16-bit C and aux
+enum { EPI_GENERIC = 0, EPI_STORE_BF16, EPI_STORE_F32, EPI_GELU, EPI_GELU_AUX, EPI_RES_BF16, EPI_RES_F32, EPI_DGELU };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -396,10 +397,12 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
   // before it, LDS-DMA and the previous batch's stores included).  bf16: 4 row blocks (32 VGPRs, two round trips per
   // tile; round 4: encoder-shape out_proj 352 -> 332 us, fc1-shaped 1240 -> 1204 us, profiles/r04_l_res_epilogue_ab.log;
   // 8 spill); fp32: 2 (32 VGPRs).
-  constexpr int RB = KIND == EPI_RES_BF16 ? 4 : (KIND == EPI_RES_F32 ? 2 : 1);
+  // (EPI_DGELU: the 16-bit pre-activation rows loaded the same way as a bf16 residual)
+  constexpr bool R16 = KIND == EPI_RES_BF16 || KIND == EPI_DGELU;
+  constexpr int RB = R16 ? 4 : (KIND == EPI_RES_F32 ? 2 : 1);
 #pragma unroll
   for (int mb = MI0; mb < FM; mb += RB) {
-  u32x4 rball[KIND == EPI_RES_BF16 ? RB : 1][FN / 2];
+  u32x4 rball[R16 ? RB : 1][FN / 2];
   f32x4 rfall[KIND == EPI_RES_F32 ? RB : 1][FN];
 #pragma unroll
   for (int q = 0; q < RB && mb + q < FM; ++q) {
@@ -409,6 +412,12 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
 #pragma unroll
       for (int np = 0; np < FN / 2; ++np)
         rball[q][np] = *(const u32x4*)(rrow + np * 32 + sw);
+    }
+    if constexpr (KIND == EPI_DGELU) {
+      const bf16* arow = p.aux + bz * p.sAux + m * p.ldaux + cw;
+#pragma unroll
+      for (int np = 0; np < FN / 2; ++np)
+        rball[q][np] = *(const u32x4*)(arow + np * 32 + sw);
     }
     if constexpr (KIND == EPI_RES_F32) {
       const float* rrow = (const float*)p.res + bz * p.sR + m * p.ldr + cw;
@@ -421,7 +430,7 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
   for (int q = 0; q < RB && mb + q < FM; ++q) {
     const int mi = mb + q;
     const int64_t m = m0 + wm * (BM / WM) + mi * 16 + li;
-    const auto& rb = rball[KIND == EPI_RES_BF16 ? q : 0];
+    const auto& rb = rball[R16 ? q : 0];
     const auto& rf = rfall[KIND == EPI_RES_F32 ? q : 0];
 #pragma unroll
     for (int np = 0; np < FN / 2; ++np) {
@@ -479,6 +488,17 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
           }
         bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
         *(u32x4*)(crow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
+      } else if constexpr (KIND == EPI_DGELU) {
+        // the generic epilogue's sequence: round the product, times gelu'(pre-activation), round
+        float x[4], y[4];
+        u4_to_pair<H>(rb[np], x, y);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[0][r] = rnd<H>((rd ? rnd<H>(v[0][r]) : v[0][r]) * gelu_grad_of<H>(x[r]));
+          v[1][r] = rnd<H>((rd ? rnd<H>(v[1][r]) : v[1][r]) * gelu_grad_of<H>(y[r]));
+        }
+        bf16* crow = (bf16*)p.C + bz * p.sC + m * p.ldc + cw;
+        *(u32x4*)(crow + np * 32 + sw) = pair_to_u4<H>(v[0], v[1]);
       } else if constexpr (KIND == EPI_RES_BF16) {
         float x[4], y[4];
         u4_to_pair<H>(rb[np], x, y);
@@ -511,11 +531,18 @@ __device__ __forceinline__ void epilogue_fast(const GemmP& p, const f32x4 (&acc)
   }
 }
 
-template <bool H, int BM, int BN, int WM, int WN, int MI0 = 0, int MI1 = -1>
+// DG: the kernel runs dX products (transposed B), the only ones with a GELU-backward epilogue
+template <bool H, int BM, int BN, int WM, int WN, int MI0 = 0, int MI1 = -1, bool DG = false>
 __device__ __forceinline__ void epilogue(const GemmP& p, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                          int n0, int wm, int wn, int lane, int bz) {
   const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
   const int k = full ? p.epi : EPI_GENERIC;
+  if constexpr (DG) {
+    if (k == EPI_DGELU) {
+      epilogue_fast<H, BM, BN, WM, WN, EPI_DGELU, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
+      return;
+    }
+  }
   if (k == EPI_STORE_BF16) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_BF16, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
   else if (k == EPI_STORE_F32) epilogue_fast<H, BM, BN, WM, WN, EPI_STORE_F32, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);
   else if (k == EPI_GELU) epilogue_fast<H, BM, BN, WM, WN, EPI_GELU, MI0, MI1>(p, acc, m0, n0, wm, wn, lane, bz);

@@ -85,6 +85,35 @@ def test_gemm_epilogues():
     assert (C4.float().cpu() - x.grad).abs().max() <= 2 ** -7 * x.grad.abs().max() + 1e-6
 
 
+@pytest.mark.parametrize("M,N,K", [(48000, 3072, 768), (1000, 768, 3072), (300, 200, 256)])
+def test_gemm_dgelu_fast_epilogue_bit_identical(M, N, K):
+    """The dX product's GELU-backward epilogue (transposed-B kernels, EPI_DGELU: the pre-activation loaded as 16-B
+    rows, round(round(acc) * gelu'(pre))) == the generic epilogue of the same product with a K-major B (the host
+    transposes W), bit for bit, and within one bf16 ulp of the fp64 value rounded at the same points.  (300, 200):
+    ragged tiles take the generic form on both paths."""
+    from tw import ops
+    g = torch.Generator().manual_seed(M + N)
+    dy = bf(torch.randn(M, K, generator=g)).to(DEV)
+    W = bf(torch.randn(K, N, generator=g) * 0.05).to(DEV)          # [N_out = K][N_in = N]: dX = dy . W
+    pre = bf(torch.randn(M, N, generator=g)).to(DEV)
+    fast = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(dy, W, fast, M, N, K, lda=K, ldb=N, ldc=N, b_trans=True, aux=pre, ldaux=N,
+             flags=ops.GEMM_ROUND | ops.GEMM_DGELU)
+    WT = W.t().contiguous()
+    gen = torch.empty_like(fast)
+    # (no split-K tail on the K-major route: the same K order as the dX kernel)
+    ops.gemm(dy, WT, gen, M, N, K, lda=K, ldb=K, ldc=N, aux=pre, ldaux=N,
+             flags=ops.GEMM_ROUND | ops.GEMM_DGELU | ops.GEMM_NOSPLIT)
+    torch.cuda.synchronize()
+    assert torch.equal(fast, gen)
+    if M <= 1000:
+        x = pre.double().cpu()
+        gp = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+        ref = bf((bf((dy.double() @ W.double()).cpu().float()).double() * gp).float()).double()
+        d = (fast.double().cpu() - ref).abs()
+        assert not bool((d > 2 ** -7 * ref.abs() + 1e-30 + 1e-4 * ref.abs().max()).any()), float(d.max())
+
+
 def _gelu_exact_bf16_bits():
     """bf16 bits of GELU for every bf16 bit pattern: PyTorch's erf-form formula in fp32 (reference),
     x * 0.5 * (1 + erf(x * M_SQRT1_2)) (the reference's autocast F.gelu), with a correctly rounded
