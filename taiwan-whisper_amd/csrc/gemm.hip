@@ -758,22 +758,29 @@ void* splitk_workspace(hipStream_t stream, size_t bytes) {
 }
 #endif
 
-// S for a dW-shaped call, 0 = no split: fewer than 512 128x128 tiles, K split into S equal chunks of
-// >= 1024 until >= 512 workgroups; fp32 output, flags within {ROUND, ACCUM}.
+int pp_grid_cus();
+
+// S for a dW-shaped call, 0 = no split: fewer than 512 128x128 tiles, K split into S equal chunks; fp32 output, flags
+// within {ROUND, ACCUM}.  The split kernel holds two workgroups per CU (64 KiB of LDS each), so a grid of
+// tiles x S workgroups runs in ceil(tiles x S / (2 x CUs)) rounds of K / S steps each: S (2..16, K % S == 0, >= 512 k
+// per chunk) minimises rounds x K / S, the smaller S on ties.  (Round 6.  Powers of two before: c2's encoder
+// 768 x 3072 weight gradients -- 144 tiles, K = 48 000 -- ran S = 4, 576 workgroups = 1.125 rounds; now S = 3, one
+// round; the decoder's 768 x 768 ones at K = 14 304 S = 12 instead of 16.  Each chunk's fp32 sum is regrouped, as any
+// split.)
 int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
   if (!a_trans || !b_trans || batch != 1 || p.c_dtype != TW_F32) return 0;
   if (p.flags & ~(F_ROUND | F_ACCUM) & 0xff) return 0;
   if ((p.N & 3) || (p.ldc & 3) || ((uintptr_t)p.C & 15)) return 0;
   const int64_t tiles = (int64_t)((p.M + 127) / 128) * ((p.N + 127) / 128);
   if (tiles >= 512) return 0;
-  // the smallest S filling 512 workgroups; where none does (few tiles, or K too short for 16 chunks), the largest S
-  // that still leaves >= 512 k per chunk (round 6: c2's decoder 768 x 768 weight gradients at K = 14 304 tokens ran
-  // unsplit on 36 workgroups, 226 us each, 36 per step; the conv-stem weight gradient on 12)
+  const int64_t slots = 2 * (int64_t)pp_grid_cus();
+  const int64_t whole = (tiles + slots - 1) / slots * p.K;          // unsplit: rounds x K
   int best = 0;
-  for (int S = 2; S <= 16; S *= 2) {
-    if (p.K % S != 0 || p.K / S < 512) break;
-    best = S;
-    if (tiles * S >= 512) break;
+  int64_t best_cost = whole;
+  for (int S = 2; S <= 16; ++S) {
+    if (p.K % S != 0 || p.K / S < 512) continue;
+    const int64_t cost = (tiles * S + slots - 1) / slots * (p.K / S);
+    if (cost < best_cost) { best_cost = cost; best = S; }
   }
   return best;
 }
