@@ -764,9 +764,9 @@ int pp_grid_cus();
 // within {ROUND, ACCUM}.  The split kernel holds two workgroups per CU (64 KiB of LDS each), so a grid of
 // tiles x S workgroups runs in ceil(tiles x S / (2 x CUs)) rounds of K / S steps each: S (2..16, K % S == 0, >= 512 k
 // per chunk) minimises rounds x K / S, the smaller S on ties.  (Round 6.  Powers of two before: c2's encoder
-// 768 x 3072 weight gradients -- 144 tiles, K = 48 000 -- ran S = 4, 576 workgroups = 1.125 rounds; now S = 3, one
-// round; the decoder's 768 x 768 ones at K = 14 304 S = 12 instead of 16.  Each chunk's fp32 sum is regrouped, as any
-// split.)
+// 768 x 3072 weight gradients -- 144 tiles, K = 48 000 -- ran S = 4, 576 workgroups = 1.125 rounds of 12 000 k; now
+// S = 10, 2.8 rounds of 4 800; the decoder's 768 x 768 ones at K = 14 304 S = 12 instead of 16.  Each chunk's fp32
+// sum is regrouped, as any split.)
 int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
   if (!a_trans || !b_trans || batch != 1 || p.c_dtype != TW_F32) return 0;
   if (p.flags & ~(F_ROUND | F_ACCUM) & 0xff) return 0;
