@@ -761,26 +761,41 @@ void* splitk_workspace(hipStream_t stream, size_t bytes) {
 int pp_grid_cus();
 
 // S for a dW-shaped call, 0 = no split: fewer than 512 128x128 tiles, K split into S equal chunks; fp32 output, flags
-// within {ROUND, ACCUM}.  The split kernel holds two workgroups per CU (64 KiB of LDS each), so a grid of
-// tiles x S workgroups runs in ceil(tiles x S / (2 x CUs)) rounds of K / S steps each: S (2..16, K % S == 0, >= 512 k
-// per chunk) minimises rounds x K / S, the smaller S on ties.  (Round 6.  Powers of two before: c2's encoder
-// 768 x 3072 weight gradients -- 144 tiles, K = 48 000 -- ran S = 4, 576 workgroups = 1.125 rounds of 12 000 k; now
-// S = 10, 2.8 rounds of 4 800; the decoder's 768 x 768 ones at K = 14 304 S = 12 instead of 16.  Each chunk's fp32
-// sum is regrouped, as any split.)
-int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans) {
+// within {ROUND, ACCUM}.  The 128x128 split kernel holds two workgroups per CU (64 KiB of LDS each), so a grid of
+// tiles x S workgroups runs in ceil(tiles x S / (2 x CUs)) rounds of K / S steps each; the 256x256 one holds one per
+// CU at R times the 128 tile's rate per CU (R = 1.4 measured from the unsplit LM-head dW against the split dW
+// products; TW_SK256_R overrides it, 0 = never), so ceil(tiles256 x S / CUs) rounds of 4 x K / S / R.  S (2..16,
+// K % S == 0, >= 512 k per chunk) and the tile minimise that, the smaller S and the 128 tile on ties.  (Round 6.
+// Powers of two before: c2's encoder 768 x 3072 weight gradients -- 144 tiles, K = 48 000 -- ran S = 4, 576
+// workgroups = 1.125 rounds of 12 000 k; with the 128 tile alone S = 10, with the 256 tile S = 6 on 216 workgroups.
+// c2 +1.3 %, c3 +0.3 % same-box, profiles/r06_al_ab.log.  Each chunk's fp32 sum is regrouped, as any split.)
+int splitk_factor(const GemmP& p, int batch, int a_trans, int b_trans, int* tile) {
+  *tile = 128;
   if (!a_trans || !b_trans || batch != 1 || p.c_dtype != TW_F32) return 0;
   if (p.flags & ~(F_ROUND | F_ACCUM) & 0xff) return 0;
   if ((p.N & 3) || (p.ldc & 3) || ((uintptr_t)p.C & 15)) return 0;
   const int64_t tiles = (int64_t)((p.M + 127) / 128) * ((p.N + 127) / 128);
   if (tiles >= 512) return 0;
-  const int64_t slots = 2 * (int64_t)pp_grid_cus();
-  const int64_t whole = (tiles + slots - 1) / slots * p.K;          // unsplit: rounds x K
+  const int64_t cus = pp_grid_cus();
+  const int64_t slots = 2 * cus;
+  // time units: one CU's 128x128 x 1k of work at the 128-tile rate.  A 128-tile round holds two workgroups per CU
+  // (2 units per k); a 256-tile round one workgroup of four times the area at R times the 128-tile rate.
+  static const double R = [] {
+    const char* e = getenv("TW_SK256_R");
+    return e ? atof(e) : 1.4;
+  }();
+  const int64_t tiles256 = (int64_t)((p.M + 255) / 256) * ((p.N + 255) / 256);
+  double best_cost = (double)((tiles + slots - 1) / slots) * 2.0 * p.K;   // unsplit: rounds x K
   int best = 0;
-  int64_t best_cost = whole;
   for (int S = 2; S <= 16; ++S) {
     if (p.K % S != 0 || p.K / S < 512) continue;
-    const int64_t cost = (tiles * S + slots - 1) / slots * (p.K / S);
-    if (cost < best_cost) { best_cost = cost; best = S; }
+    const double kc = (double)(p.K / S);
+    const double c128 = (double)((tiles * S + slots - 1) / slots) * 2.0 * kc;
+    if (c128 < best_cost) { best_cost = c128; best = S; *tile = 128; }
+    if (R > 0) {
+      const double c256 = (double)((tiles256 * S + cus - 1) / cus) * 4.0 * kc / R;
+      if (c256 < best_cost) { best_cost = c256; best = S; *tile = 256; }
+    }
   }
   return best;
 }
@@ -1083,7 +1098,8 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
     return TW_OK;
   }
   if (!(flags & (16384 | 256 | 512 | 1024 | 2048))) {   // 16384: no split-K; forced tiles: A/B runs
-    const int S = splitk_factor(p, batch, a_trans, b_trans);
+    int sk_tile = 128;
+    const int S = splitk_factor(p, batch, a_trans, b_trans, &sk_tile);
     const size_t bytes = (size_t)S * M * N * sizeof(float);
     void* ws = (S > 0 && bytes <= ((size_t)1 << 30)) ? splitk_workspace(stream, bytes) : nullptr;
     if (ws) {
@@ -1095,7 +1111,8 @@ int gemm_run(const void* A, int64_t lda, int a_trans, const void* B, int64_t ldb
       q.C = ws; q.ldc = N; q.sC = (int64_t)M * N; q.c_dtype = TW_F32;
       q.alpha = 1.f; q.flags = 0; q.bias = nullptr; q.res = nullptr; q.aux = nullptr;
       q.epi = pick_epilogue(q, S);
-      launch<H, true, true, 128, 128, 2, 2, 2>(q, S, stream);
+      if (sk_tile == 256) launch<H, true, true, 256, 256, 2, 4, 2>(q, S, stream);
+      else launch<H, true, true, 128, 128, 2, 2, 2>(q, S, stream);
       TW_CHECK_LAUNCH();
       const int64_t work = (int64_t)M * (N / 4);
       const int grid = (int)std::min<int64_t>((work + 255) / 256, 4096);
